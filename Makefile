@@ -1,0 +1,33 @@
+# Top-level build: the gfx950 product library, the oracle, the reference build.
+#   make            libmtcp_gpu.so + oracle/libmtcp_oracle.so
+#   make ref        oracle/_ref (needs /root/reference; this container only)
+#   make golden     regenerate tests/golden from the reference
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
+LIB      := mtcp_amd/lib/libmtcp_gpu.so
+SRCS     := mtcp_amd/csrc/mtcp_gpu.hip mtcp_amd/csrc/pktgen.hip
+DEPS     := $(SRCS) mtcp_amd/csrc/rx_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h
+
+.PHONY: all lib oracle ref golden examples clean
+
+all: lib oracle
+
+lib: $(LIB)
+
+$(LIB): $(DEPS)
+	mkdir -p mtcp_amd/lib
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+
+oracle:
+	$(MAKE) -C oracle
+
+ref:
+	$(MAKE) -C oracle ref
+
+golden:
+	$(MAKE) -C oracle golden
+
+clean:
+	rm -f $(LIB)
+	$(MAKE) -C oracle clean

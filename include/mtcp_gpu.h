@@ -1,0 +1,238 @@
+/*
+ * mtcp_gpu.h — C ABI of the MI355X (gfx950) rx/tx checksum, parse and RSS
+ * offload for mTCP's software (--disable-hwcsum) per-packet path.
+ *
+ * Plain C, no HIP or C++ types: a libmtcp built with
+ * `gcc -O3 -fgnu89-inline -Werror` (mtcp/src/Makefile.in:20-31) includes this
+ * header and links libmtcp_gpu.so.  Every entry point returns 0 or a negative
+ * errno-style code (MTCP_GPU_E*); nothing here calls exit() or throws.
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * mTCP tree):
+ *
+ *   mtcp_gpu_rx_chunk / _rx_chunk_dev
+ *       the per-packet loop of RunMainLoop (mtcp/src/core.c:768-776), i.e.
+ *       get_rptr (mtcp/src/include/io_module.h:62) + ProcessPacket
+ *       (mtcp/src/eth_in.c:9-56) → ProcessIPv4Packet (mtcp/src/ip_in.c:15-62)
+ *       → the head of ProcessTCPPacket (mtcp/src/tcp_in.c:1138-1175), run for
+ *       a whole PSIO-style chunk (io_engine/include/ps.h:181-200) at once.
+ *       Inside, ip_fast_csum (io_engine/include/ps.h:66-95) and
+ *       TCPCalcChecksum (mtcp/src/tcp_util.c:157-190) are evaluated for every
+ *       packet, and optionally GetRSSHash / GetRSSCPUCore
+ *       (util/rss.c:107-165, mtcp/src/rss.c:44-103).
+ *   mtcp_gpu_rx_ptrs / _rx_ptrs_dev
+ *       the same for a DPDK/netmap style burst of (pointer, len) pairs
+ *       (dpdk_get_rptr mtcp/src/dpdk_module.c:454-485,
+ *        netmap_get_rptr mtcp/src/netmap_module.c:193-200).
+ *   mtcp_gpu_tx_fill / _tx_fill_dev
+ *       the DISABLE_HWCSUM checksum fills of the tx path:
+ *       iph->check = ip_fast_csum(iph, iph->ihl)   (mtcp/src/ip_out.c:94,164)
+ *       tcph->check = TCPCalcChecksum(...)          (mtcp/src/tcp_out.c:211,329)
+ *   mtcp_gpu_dev_ioctl
+ *       io_module_func.dev_ioctl (mtcp/src/include/io_module.h:67) for the
+ *       checksum commands PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM / PKT_TX_IP_CSUM /
+ *       PKT_TX_TCPIP_CSUM (io_module.h:80-87): 0 = "the device does it",
+ *       -1 = "do it in software", the contract of dpdk_dev_ioctl
+ *       (mtcp/src/dpdk_module.c:809-816).
+ *
+ * Ownership: packet memory belongs to the caller (the I/O module) and is
+ * never retained past a call; rx never writes packets (the reference's
+ * `tcph->check = 0` on a bad TCP checksum, tcp_in.c:1171, is reported through
+ * the verdict only); results belong to the caller.
+ *
+ * Threading: one context per mTCP thread (mtcp/src/core.c:1057 pins one
+ * thread per core); a context owns one HIP stream and its staging buffers and
+ * is not re-entrant.  Distinct contexts may be used concurrently.
+ */
+#ifndef MTCP_GPU_H
+#define MTCP_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTCP_GPU_ABI_VERSION 1
+
+/* ---- error codes (negative returns) ----------------------------------- */
+#define MTCP_GPU_OK        0
+#define MTCP_GPU_EINVAL   (-22)  /* bad argument (NULL, misaligned, too big) */
+#define MTCP_GPU_ENOMEM   (-12)  /* device or pinned host allocation failed  */
+#define MTCP_GPU_ENODEV   (-19)  /* no such HIP device / no GPU              */
+#define MTCP_GPU_EIO       (-5)  /* HIP runtime error during the call        */
+
+/* ---- dev_ioctl commands: same values as mtcp/src/include/io_module.h:80-87 */
+#define MTCP_GPU_PKT_TX_IP_CSUM          0x01
+#define MTCP_GPU_PKT_TX_TCP_CSUM         0x02
+#define MTCP_GPU_PKT_RX_TCP_LROSEG       0x03
+#define MTCP_GPU_PKT_TX_TCPIP_CSUM       0x04
+#define MTCP_GPU_PKT_RX_IP_CSUM          0x05
+#define MTCP_GPU_PKT_RX_TCP_CSUM         0x06
+#define MTCP_GPU_PKT_TX_TCPIP_CSUM_PEEK  0x07
+#define MTCP_GPU_DRV_NAME                0x08
+
+/* ---- open flags -------------------------------------------------------- */
+#define MTCP_GPU_F_RSS           0x1u  /* compute rss_hash / rss_queue per packet */
+#define MTCP_GPU_F_RSS_ENDIAN    0x2u  /* GetRSSCPUCore endian fix (util/rss.c:161-162;
+                                          mtcp/src/rss.c:96-99 endian_check) */
+
+/*
+ * Packet descriptor of a contiguous chunk.  Layout-compatible with PSIO's
+ * struct ps_pkt_info {uint32_t offset; uint16_t len; uint8_t checksum_rx;}
+ * (io_engine/include/ps.h:181-185), so a ps_chunk's info[] array can be
+ * passed as is with off_shift = 0.  With off_shift = 6 the offset counts 64 B
+ * units (PSIO aligns packets to 64 B, io_engine/lib/pslib.c:146), which
+ * reaches 256 GiB chunks.  Byte offset = offset << off_shift; it must be a
+ * multiple of 4 and offset + len must lie inside the chunk, otherwise the
+ * packet gets MTCP_GPU_V_BAD_DESC and is not read.
+ * len = frame length as get_rptr's *len (Ethernet header through the end of
+ * the frame, CRC stripped; mtcp/src/dpdk_module.c:467).
+ */
+typedef struct mtcp_gpu_desc {
+    uint32_t offset;
+    uint16_t len;
+    uint8_t  flags;      /* ignored (ps_pkt_info.checksum_rx) */
+    uint8_t  rsvd;
+} mtcp_gpu_desc;
+
+/* Per-packet verdict: one value per exit of the reference's rx chain. */
+enum mtcp_gpu_verdict {
+    MTCP_GPU_V_TCP_OK         = 0,  /* checksums good, reached StreamHTSearch (tcp_in.c:1186) */
+    MTCP_GPU_V_ETH_OTHER      = 1,  /* not IPv4/ARP: release, TRUE        (eth_in.c:43-46) */
+    MTCP_GPU_V_ARP            = 2,  /* h_proto 0x0806                     (eth_in.c:39-41) */
+    MTCP_GPU_V_IP_SHORT       = 3,  /* tot_len < 20, ERROR                (ip_in.c:25-26)  */
+    MTCP_GPU_V_IP_CSUM_BAD    = 4,  /* ip_fast_csum != 0, ERROR           (ip_in.c:35-36)  */
+    MTCP_GPU_V_IP_VERSION     = 5,  /* version != 4, release, FALSE       (ip_in.c:47-50)  */
+    MTCP_GPU_V_ICMP           = 6,  /* protocol 1 -> ProcessICMPPacket    (ip_in.c:55-56)  */
+    MTCP_GPU_V_IP_PROTO_OTHER = 7,  /* other protocol, FALSE              (ip_in.c:57-59)  */
+    MTCP_GPU_V_TCP_LEN_BAD    = 8,  /* tot_len < 4*(ihl+doff), ERROR      (tcp_in.c:1155-1156) */
+    MTCP_GPU_V_TCP_CSUM_BAD   = 9,  /* TCPCalcChecksum != 0, ERROR; the reference also
+                                       sets tcph->check = 0               (tcp_in.c:1167-1173) */
+    MTCP_GPU_V_TRUNCATED      = 10, /* the reference would read past len here (undefined) */
+    MTCP_GPU_V_BAD_DESC       = 11  /* descriptor outside the chunk or misaligned */
+};
+
+/* ProcessPacket's `ret < 0` (eth_in.c:49-53): the verdicts counted in
+ * nstat.rx_errors. */
+#define MTCP_GPU_VERDICT_IS_RX_ERROR(v) \
+    ((v) == MTCP_GPU_V_IP_SHORT || (v) == MTCP_GPU_V_IP_CSUM_BAD || \
+     (v) == MTCP_GPU_V_TCP_LEN_BAD || (v) == MTCP_GPU_V_TCP_CSUM_BAD)
+
+/*
+ * Per-packet result, 40 B.  A field is written only once the reference's
+ * rx chain has read it; everything else is 0.  Byte orders follow the
+ * reference's own variables.
+ */
+typedef struct mtcp_gpu_result {
+    uint32_t saddr;       /*  0 iph->saddr, as in memory (network order)       */
+    uint32_t daddr;       /*  4 iph->daddr, as in memory                       */
+    uint16_t sport;       /*  8 tcph->source, as in memory                     */
+    uint16_t dport;       /* 10 tcph->dest, as in memory                       */
+    uint32_t seq;         /* 12 ntohl(tcph->seq)        tcp_in.c:1147          */
+    uint32_t ack_seq;     /* 16 ntohl(tcph->ack_seq)    tcp_in.c:1148          */
+    uint16_t window;      /* 20 ntohs(tcph->window)     tcp_in.c:1149          */
+    uint16_t ip_len;      /* 22 ntohs(iph->tot_len)     ip_in.c:21             */
+    uint16_t ip_csum;     /* 24 ip_fast_csum(iph, ihl)  ip_in.c:35 (0 = good)  */
+    uint16_t tcp_csum;    /* 26 TCPCalcChecksum(...)    tcp_in.c:1165 (0 = good) */
+    uint32_t rss_hash;    /* 28 GetRSSHash(ntohl(saddr), ntohl(daddr),
+                                           ntohs(sport), ntohs(dport))         */
+    uint16_t payload_len; /* 32 ip_len - 4*(ihl+doff)   tcp_in.c:1144          */
+    uint8_t  ihl_doff;    /* 34 ihl | doff << 4                                */
+    uint8_t  tcp_flags;   /* 35 FIN 0x01 SYN 0x02 RST 0x04 PSH 0x08 ACK 0x10 URG 0x20 */
+    uint8_t  verdict;     /* 36 enum mtcp_gpu_verdict                          */
+    uint8_t  rss_queue;   /* 37 GetRSSCPUCore(...) queue                       */
+    uint16_t eth_type;    /* 38 ntohs(ethh->h_proto)    eth_in.c:13            */
+} mtcp_gpu_result;
+
+typedef struct mtcp_gpu_ctx mtcp_gpu_ctx;
+
+/* Library / device introspection. */
+int         mtcp_gpu_abi_version(void);
+const char *mtcp_gpu_strerror(int err);
+int         mtcp_gpu_device_count(void);
+
+/*
+ * Open a context on HIP device `device`.
+ *   rss_key        40-byte Toeplitz key (util/rss.c:84-90 layout); NULL selects
+ *                  the reference's active key, 0x05 x 40 (util/rss.c:84-90).
+ *   rss_num_queues queue count for rss_queue (>= 1; ignored without F_RSS).
+ *   flags          MTCP_GPU_F_*.
+ */
+int  mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key,
+                   int rss_num_queues, uint32_t flags);
+void mtcp_gpu_close(mtcp_gpu_ctx *ctx);
+
+/* dev_ioctl-compatible capability answer (0 = offloaded, -1 = software). */
+int  mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp);
+
+/* The HIP stream the context launches on (a hipStream_t, as void*). */
+void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx);
+
+/*
+ * Device-resident rx: chunk, descriptors and results are device (or
+ * device-mapped) memory.  Asynchronous on `stream` (a hipStream_t; NULL =
+ * the context's stream).  buf_len must be a multiple of 16.
+ */
+int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
+                          const mtcp_gpu_desc *d_desc, uint32_t n,
+                          uint32_t off_shift, mtcp_gpu_result *d_out,
+                          void *stream);
+
+/*
+ * Device-resident rx over a pointer burst.  d_pkts[i] is a device-accessible
+ * address (device memory, or host memory registered with
+ * mtcp_gpu_host_register: the kernel then reads it over PCIe, zero copy),
+ * 4-byte aligned; d_lens[i] its frame length.
+ */
+int mtcp_gpu_rx_ptrs_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts,
+                         const uint16_t *d_lens, uint32_t n,
+                         mtcp_gpu_result *d_out, void *stream);
+
+/*
+ * Host-memory rx (the drop-in for the rx loop): chunk and descriptors in host
+ * memory, results written to host memory; synchronous.  Large chunks are
+ * streamed H2D -> kernel -> D2H through pinned staging on several streams;
+ * register the chunk with mtcp_gpu_host_register for full PCIe rate.
+ * Descriptor offsets must be non-decreasing for the streamed path (PSIO
+ * chunks are); otherwise the chunk is staged whole.
+ */
+int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
+                      const mtcp_gpu_desc *desc, uint32_t n, uint32_t off_shift,
+                      mtcp_gpu_result *out);
+
+/* Host-memory rx of a pointer burst (gathered into pinned staging). */
+int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts,
+                     const uint16_t *lens, uint32_t n, mtcp_gpu_result *out);
+
+/*
+ * tx checksum fill, in place: for every well-formed IPv4/TCP frame
+ * (eth 0x0800, version 4, ihl >= 5, protocol 6, doff >= 5,
+ * 4*(ihl+doff) <= tot_len, 14 + tot_len <= len) write
+ *   iph->check  = ip_fast_csum(iph, ihl)      computed with check = 0
+ *   tcph->check = TCPCalcChecksum(tcph, tot_len - 4*ihl, saddr, daddr)
+ *                                             computed with check = 0
+ * Other frames are left untouched.  *n_filled (may be NULL) receives the
+ * number of frames written (host variant only).
+ */
+int mtcp_gpu_tx_fill_dev(mtcp_gpu_ctx *ctx, void *d_buf, uint64_t buf_len,
+                         const mtcp_gpu_desc *d_desc, uint32_t n,
+                         uint32_t off_shift, void *stream);
+int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len,
+                     const mtcp_gpu_desc *desc, uint32_t n, uint32_t off_shift,
+                     uint32_t *n_filled);
+
+/* Pin / unpin host memory for DMA and zero-copy device access
+ * (hipHostRegister; the pattern SURVEY §7 names for DPDK mempools). */
+int mtcp_gpu_host_register(void *ptr, uint64_t len);
+int mtcp_gpu_host_unregister(void *ptr);
+
+/* Synchronise the context's stream. */
+int mtcp_gpu_sync(mtcp_gpu_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MTCP_GPU_H */

@@ -1,0 +1,19 @@
+"""numpy views of the C ABI records (include/mtcp_gpu.h)."""
+import numpy as np
+
+# struct mtcp_gpu_desc: layout-compatible with PSIO's ps_pkt_info (ps.h:181-185)
+DESC_DTYPE = np.dtype([("offset", "<u4"), ("len", "<u2"), ("flags", "u1"), ("rsvd", "u1")])
+
+# struct mtcp_gpu_result (40 B)
+RESULT_DTYPE = np.dtype([
+    ("saddr", "<u4"), ("daddr", "<u4"), ("sport", "<u2"), ("dport", "<u2"),
+    ("seq", "<u4"), ("ack_seq", "<u4"), ("window", "<u2"), ("ip_len", "<u2"),
+    ("ip_csum", "<u2"), ("tcp_csum", "<u2"), ("rss_hash", "<u4"),
+    ("payload_len", "<u2"), ("ihl_doff", "u1"), ("tcp_flags", "u1"),
+    ("verdict", "u1"), ("rss_queue", "u1"), ("eth_type", "<u2"),
+])
+assert DESC_DTYPE.itemsize == 8 and RESULT_DTYPE.itemsize == 40
+
+VERDICTS = ("TCP_OK", "ETH_OTHER", "ARP", "IP_SHORT", "IP_CSUM_BAD", "IP_VERSION", "ICMP",
+            "IP_PROTO_OTHER", "TCP_LEN_BAD", "TCP_CSUM_BAD", "TRUNCATED", "BAD_DESC")
+RX_ERROR_VERDICTS = (3, 4, 8, 9)   # ProcessPacket ret < 0 (eth_in.c:49-53)

@@ -1,0 +1,454 @@
+// mtcp_gpu.hip — the C ABI of include/mtcp_gpu.h: contexts, launches and the
+// host-memory pipelines around the gfx950 kernels of rx_kernels.hpp.
+//
+// Product code only: there is no CPU fallback here.  When no GPU is usable
+// every entry point returns an error code, and the caller (mTCP) keeps its
+// software path exactly as dev_ioctl returning -1 would make it
+// (mtcp/src/ip_in.c:29-31, tcp_in.c:1160-1164).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+
+#include "../../include/mtcp_gpu.h"
+#include "rx_kernels.hpp"
+
+namespace {
+
+constexpr int kStages = 3;                       // H2D | kernel | D2H overlap
+constexpr uint64_t kStageBytes = 64ull << 20;    // chunk bytes per pipeline stage
+constexpr uint32_t kStagePkts = 1u << 16;        // descriptors per pipeline stage
+
+struct Stage {
+    uint8_t *d_buf = nullptr;
+    mtcp_gpu_desc *d_desc = nullptr;
+    mtcp_gpu_result *d_out = nullptr;
+    uint64_t buf_cap = 0;
+    uint32_t pkt_cap = 0;
+    hipStream_t stream = nullptr;
+};
+
+}  // namespace
+
+struct mtcp_gpu_ctx {
+    int device = 0;
+    int num_cu = 256;
+    uint32_t flags = 0;
+    uint32_t rss_nq = 1;
+    uint32_t rss_endian = 0;
+    hipStream_t stream = nullptr;
+    uint32_t *d_rss_tables = nullptr;
+    uint32_t *d_count = nullptr;
+    Stage stage[kStages];
+    uint8_t *h_gather = nullptr;                 // pinned, for rx_ptrs
+    uint64_t h_gather_cap = 0;
+    mtcp_gpu_desc *h_gather_desc = nullptr;
+    uint32_t h_gather_desc_cap = 0;
+};
+
+namespace {
+
+#define HIP_OK(x) ((x) == hipSuccess)
+
+// util/rss.c:13-105 (BuildKeyCache), then the 12 byte tables the kernel XORs:
+// table[t][v] = XOR of cache[8t + m] over the bits of v, MSB first.
+void build_rss_tables(const uint8_t key[40], uint32_t *tables) {
+    uint32_t cache[96];
+    uint32_t result = ((uint32_t)key[0] << 24) | ((uint32_t)key[1] << 16) |
+                      ((uint32_t)key[2] << 8) | (uint32_t)key[3];
+    uint32_t idx = 32;
+    for (int i = 0; i < 96; i++, idx++) {
+        cache[i] = result;
+        const uint32_t bit = ((key[idx / 8] << (idx % 8)) & 0x80) ? 1u : 0u;
+        result = (result << 1) | bit;
+    }
+    for (int t = 0; t < 12; ++t)
+        for (int v = 0; v < 256; ++v) {
+            uint32_t h = 0;
+            for (int m = 0; m < 8; ++m)
+                if (v & (0x80 >> m)) h ^= cache[8 * t + m];
+            tables[t * 256 + v] = h;
+        }
+}
+
+uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
+    const uint32_t groups = (n + mg::kWave - 1) / mg::kWave;
+    const uint32_t blocks = (groups + mg::kWavesPerBlock - 1) / mg::kWavesPerBlock;
+    const uint32_t cap = (uint32_t)ctx->num_cu * 8;
+    return std::max(1u, std::min(blocks, cap));
+}
+
+template <int MODE>
+int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
+    if (kp.n == 0) return MTCP_GPU_OK;
+    const dim3 grid(grid_for(ctx, kp.n)), block(mg::kBlock);
+    const bool rss = MODE != mg::kTxChunk && (ctx->flags & MTCP_GPU_F_RSS);
+    if (rss)
+        hipLaunchKernelGGL((mg::rx_kernel<MODE, true>), grid, block, 0, st, kp);
+    else
+        hipLaunchKernelGGL((mg::rx_kernel<MODE, false>), grid, block, 0, st, kp);
+    return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
+}
+
+mg::KParams base_params(mtcp_gpu_ctx *ctx) {
+    mg::KParams kp{};
+    kp.rss_tables = ctx->d_rss_tables;
+    kp.rss_nq = ctx->rss_nq;
+    kp.rss_endian = ctx->rss_endian;
+    return kp;
+}
+
+hipStream_t pick(mtcp_gpu_ctx *ctx, void *stream) {
+    return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+int stage_reserve(Stage &s, uint64_t bytes, uint32_t pkts) {
+    if (bytes > s.buf_cap) {
+        if (s.d_buf) (void)hipFree(s.d_buf);
+        s.d_buf = nullptr;
+        s.buf_cap = 0;
+        const uint64_t cap = (bytes + 4095) & ~4095ull;
+        if (!HIP_OK(hipMalloc(&s.d_buf, cap))) return MTCP_GPU_ENOMEM;
+        s.buf_cap = cap;
+    }
+    if (pkts > s.pkt_cap) {
+        if (s.d_desc) (void)hipFree(s.d_desc);
+        if (s.d_out) (void)hipFree(s.d_out);
+        s.d_desc = nullptr;
+        s.d_out = nullptr;
+        s.pkt_cap = 0;
+        if (!HIP_OK(hipMalloc(&s.d_desc, (size_t)pkts * sizeof(mtcp_gpu_desc))) ||
+            !HIP_OK(hipMalloc(&s.d_out, (size_t)pkts * sizeof(mtcp_gpu_result))))
+            return MTCP_GPU_ENOMEM;
+        s.pkt_cap = pkts;
+    }
+    return MTCP_GPU_OK;
+}
+
+bool offsets_sorted(const mtcp_gpu_desc *desc, uint32_t n) {
+    for (uint32_t i = 1; i < n; ++i)
+        if (desc[i].offset < desc[i - 1].offset) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mtcp_gpu_abi_version(void) { return MTCP_GPU_ABI_VERSION; }
+
+const char *mtcp_gpu_strerror(int err) {
+    switch (err) {
+        case MTCP_GPU_OK: return "success";
+        case MTCP_GPU_EINVAL: return "invalid argument";
+        case MTCP_GPU_ENOMEM: return "out of device or pinned host memory";
+        case MTCP_GPU_ENODEV: return "no usable HIP device";
+        case MTCP_GPU_EIO: return "HIP runtime error";
+        default: return "unknown error";
+    }
+}
+
+int mtcp_gpu_device_count(void) {
+    int n = 0;
+    if (!HIP_OK(hipGetDeviceCount(&n))) return 0;
+    return n;
+}
+
+int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rss_num_queues,
+                  uint32_t flags) {
+    static const uint8_t key05[40] = {
+        5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5,
+        5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5};
+    if (!out) return MTCP_GPU_EINVAL;
+    *out = nullptr;
+    if ((flags & MTCP_GPU_F_RSS) && rss_num_queues < 1) return MTCP_GPU_EINVAL;
+    int ndev = 0;
+    if (!HIP_OK(hipGetDeviceCount(&ndev)) || device < 0 || device >= ndev) return MTCP_GPU_ENODEV;
+    if (!HIP_OK(hipSetDevice(device))) return MTCP_GPU_ENODEV;
+
+    mtcp_gpu_ctx *ctx = new (std::nothrow) mtcp_gpu_ctx();
+    if (!ctx) return MTCP_GPU_ENOMEM;
+    ctx->device = device;
+    ctx->flags = flags;
+    ctx->rss_nq = (uint32_t)std::max(1, rss_num_queues);
+    ctx->rss_endian = (flags & MTCP_GPU_F_RSS_ENDIAN) ? 1u : 0u;
+    hipDeviceProp_t prop;
+    if (HIP_OK(hipGetDeviceProperties(&prop, device)) && prop.multiProcessorCount > 0)
+        ctx->num_cu = prop.multiProcessorCount;
+
+    uint32_t tables[mg::kRssTableWords];
+    build_rss_tables(rss_key ? rss_key : key05, tables);
+    int rc = MTCP_GPU_OK;
+    if (!HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) ||
+        !HIP_OK(hipMalloc(&ctx->d_rss_tables, sizeof(tables))) ||
+        !HIP_OK(hipMalloc(&ctx->d_count, sizeof(uint32_t))) ||
+        !HIP_OK(hipMemcpy(ctx->d_rss_tables, tables, sizeof(tables), hipMemcpyHostToDevice)))
+        rc = MTCP_GPU_ENOMEM;
+    for (int s = 0; s < kStages && rc == MTCP_GPU_OK; ++s)
+        if (!HIP_OK(hipStreamCreateWithFlags(&ctx->stage[s].stream, hipStreamNonBlocking)))
+            rc = MTCP_GPU_EIO;
+    if (rc != MTCP_GPU_OK) {
+        mtcp_gpu_close(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return MTCP_GPU_OK;
+}
+
+void mtcp_gpu_close(mtcp_gpu_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto &s : ctx->stage) {
+        if (s.stream) {
+            (void)hipStreamSynchronize(s.stream);
+            (void)hipStreamDestroy(s.stream);
+        }
+        if (s.d_buf) (void)hipFree(s.d_buf);
+        if (s.d_desc) (void)hipFree(s.d_desc);
+        if (s.d_out) (void)hipFree(s.d_out);
+    }
+    if (ctx->h_gather) (void)hipHostFree(ctx->h_gather);
+    if (ctx->h_gather_desc) (void)hipHostFree(ctx->h_gather_desc);
+    if (ctx->d_rss_tables) (void)hipFree(ctx->d_rss_tables);
+    if (ctx->d_count) (void)hipFree(ctx->d_count);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp) {
+    (void)nif;
+    (void)argp;
+    if (!ctx) return -1;
+    switch (cmd) {   // the commands this device computes (dpdk_module.c:809-816 contract)
+        case MTCP_GPU_PKT_RX_IP_CSUM:
+        case MTCP_GPU_PKT_RX_TCP_CSUM:
+        case MTCP_GPU_PKT_TX_IP_CSUM:
+        case MTCP_GPU_PKT_TX_TCPIP_CSUM:
+            return 0;
+        default:
+            return -1;
+    }
+}
+
+void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int mtcp_gpu_sync(mtcp_gpu_ctx *ctx) {
+    if (!ctx) return MTCP_GPU_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    return HIP_OK(hipStreamSynchronize(ctx->stream)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
+}
+
+int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
+                          const mtcp_gpu_desc *d_desc, uint32_t n, uint32_t off_shift,
+                          mtcp_gpu_result *d_out, void *stream) {
+    if (!ctx || (n && (!d_buf || !d_desc || !d_out)) || off_shift > 16 || (buf_len & 15) ||
+        ((uintptr_t)d_buf & 15) || ((uintptr_t)d_out & 7) || ((uintptr_t)d_desc & 7))
+        return MTCP_GPU_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    mg::KParams kp = base_params(ctx);
+    kp.buf = static_cast<const uint8_t *>(d_buf);
+    kp.buf_len = buf_len;
+    kp.desc = d_desc;
+    kp.n = n;
+    kp.off_shift = off_shift;
+    kp.out = d_out;
+    return launch<mg::kRxChunk>(ctx, kp, pick(ctx, stream));
+}
+
+int mtcp_gpu_rx_ptrs_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts, const uint16_t *d_lens,
+                         uint32_t n, mtcp_gpu_result *d_out, void *stream) {
+    if (!ctx || (n && (!d_pkts || !d_lens || !d_out)) || ((uintptr_t)d_out & 7))
+        return MTCP_GPU_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    mg::KParams kp = base_params(ctx);
+    kp.ptrs = d_pkts;
+    kp.lens = d_lens;
+    kp.n = n;
+    kp.out = d_out;
+    return launch<mg::kRxPtrs>(ctx, kp, pick(ctx, stream));
+}
+
+int mtcp_gpu_tx_fill_dev(mtcp_gpu_ctx *ctx, void *d_buf, uint64_t buf_len,
+                         const mtcp_gpu_desc *d_desc, uint32_t n, uint32_t off_shift,
+                         void *stream) {
+    if (!ctx || (n && (!d_buf || !d_desc)) || off_shift > 16 || (buf_len & 15) ||
+        ((uintptr_t)d_buf & 15) || ((uintptr_t)d_desc & 7))
+        return MTCP_GPU_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    mg::KParams kp = base_params(ctx);
+    kp.buf = static_cast<const uint8_t *>(d_buf);
+    kp.buf_len = buf_len;
+    kp.desc = d_desc;
+    kp.n = n;
+    kp.off_shift = off_shift;
+    return launch<mg::kTxChunk>(ctx, kp, pick(ctx, stream));
+}
+
+// Host-memory rx: batches of packets stream through kStages pinned-device
+// stages, each on its own stream (H2D of batch b+1 overlaps the kernel of b
+// and the D2H of b-1).  Each batch copies only the byte span its packets
+// occupy and the kernel rebases descriptor offsets by that span's start.
+int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
+                      const mtcp_gpu_desc *desc, uint32_t n, uint32_t off_shift,
+                      mtcp_gpu_result *out) {
+    if (!ctx || (n && (!buf || !desc || !out)) || off_shift > 16) return MTCP_GPU_EINVAL;
+    if (n == 0) return MTCP_GPU_OK;
+    (void)hipSetDevice(ctx->device);
+    int rc = MTCP_GPU_OK;
+    if (!offsets_sorted(desc, n)) {
+        // arbitrary order: stage the whole chunk once, then batches of descriptors
+        Stage &s = ctx->stage[0];
+        rc = stage_reserve(s, ((buf_len + 15) & ~15ull) + 16, kStagePkts);
+        if (rc == MTCP_GPU_OK &&
+            !HIP_OK(hipMemcpyAsync(s.d_buf, buf, buf_len, hipMemcpyHostToDevice, s.stream)))
+            rc = MTCP_GPU_EIO;
+        for (uint32_t first = 0; first < n && rc == MTCP_GPU_OK; first += kStagePkts) {
+            const uint32_t cnt = std::min(n - first, kStagePkts);
+            mg::KParams kp = base_params(ctx);
+            kp.buf = s.d_buf;
+            kp.buf_len = buf_len;
+            kp.desc = s.d_desc;
+            kp.n = cnt;
+            kp.off_shift = off_shift;
+            kp.out = s.d_out;
+            if (!HIP_OK(hipMemcpyAsync(s.d_desc, desc + first, (size_t)cnt * sizeof(mtcp_gpu_desc),
+                                       hipMemcpyHostToDevice, s.stream)))
+                rc = MTCP_GPU_EIO;
+            if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream);
+            if (rc == MTCP_GPU_OK &&
+                !HIP_OK(hipMemcpyAsync(out + first, s.d_out, (size_t)cnt * sizeof(mtcp_gpu_result),
+                                       hipMemcpyDeviceToHost, s.stream)))
+                rc = MTCP_GPU_EIO;
+        }
+    } else {
+        uint32_t first = 0;
+        for (int b = 0; first < n && rc == MTCP_GPU_OK; ++b) {
+            // grow the batch while its byte span fits one stage
+            const uint64_t lo = std::min(((uint64_t)desc[first].offset << off_shift) & ~15ull,
+                                         buf_len & ~15ull);
+            uint64_t hi = lo;
+            uint32_t cnt = 0;
+            while (first + cnt < n && cnt < kStagePkts) {
+                const uint64_t p = (uint64_t)desc[first + cnt].offset << off_shift;
+                const uint64_t end = std::max(std::min(p + desc[first + cnt].len, buf_len), lo);
+                if (cnt > 0 && std::max(hi, end) - lo > kStageBytes) break;
+                hi = std::max(hi, end);
+                ++cnt;
+            }
+            Stage &s = ctx->stage[b % kStages];
+            const uint64_t span = hi - lo;
+            rc = stage_reserve(s, ((span + 15) & ~15ull) + 16, kStagePkts);
+            if (rc != MTCP_GPU_OK) break;
+            mg::KParams kp = base_params(ctx);
+            kp.buf = s.d_buf;
+            kp.buf_len = span;           // descriptors are bounded by the caller's buf_len
+            kp.base_sub = (int64_t)lo;
+            kp.desc = s.d_desc;
+            kp.n = cnt;
+            kp.off_shift = off_shift;
+            kp.out = s.d_out;
+            if ((span && !HIP_OK(hipMemcpyAsync(s.d_buf, buf + lo, span, hipMemcpyHostToDevice,
+                                                s.stream))) ||
+                !HIP_OK(hipMemcpyAsync(s.d_desc, desc + first, (size_t)cnt * sizeof(mtcp_gpu_desc),
+                                       hipMemcpyHostToDevice, s.stream)))
+                rc = MTCP_GPU_EIO;
+            if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream);
+            if (rc == MTCP_GPU_OK &&
+                !HIP_OK(hipMemcpyAsync(out + first, s.d_out, (size_t)cnt * sizeof(mtcp_gpu_result),
+                                       hipMemcpyDeviceToHost, s.stream)))
+                rc = MTCP_GPU_EIO;
+            first += cnt;
+        }
+    }
+    for (auto &s : ctx->stage)
+        if (s.stream && !HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK)
+            rc = MTCP_GPU_EIO;
+    return rc;
+}
+
+int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *lens,
+                     uint32_t n, mtcp_gpu_result *out) {
+    if (!ctx || (n && (!pkts || !lens || !out))) return MTCP_GPU_EINVAL;
+    if (n == 0) return MTCP_GPU_OK;
+    (void)hipSetDevice(ctx->device);
+    // gather into a pinned PSIO-style chunk (64 B aligned slots, pslib.c:146)
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += ((uint64_t)lens[i] + 63) & ~63ull;
+    if (total > ctx->h_gather_cap) {
+        if (ctx->h_gather) (void)hipHostFree(ctx->h_gather);
+        ctx->h_gather = nullptr;
+        ctx->h_gather_cap = 0;
+        if (!HIP_OK(hipHostMalloc(&ctx->h_gather, total, hipHostMallocDefault))) return MTCP_GPU_ENOMEM;
+        ctx->h_gather_cap = total;
+    }
+    if (n > ctx->h_gather_desc_cap) {
+        if (ctx->h_gather_desc) (void)hipHostFree(ctx->h_gather_desc);
+        ctx->h_gather_desc = nullptr;
+        ctx->h_gather_desc_cap = 0;
+        if (!HIP_OK(hipHostMalloc(&ctx->h_gather_desc, (size_t)n * sizeof(mtcp_gpu_desc),
+                                  hipHostMallocDefault)))
+            return MTCP_GPU_ENOMEM;
+        ctx->h_gather_desc_cap = n;
+    }
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        mtcp_gpu_desc &d = ctx->h_gather_desc[i];
+        d.offset = (uint32_t)(off >> 6);
+        d.len = lens[i];
+        d.flags = d.rsvd = 0;
+        if (pkts[i]) memcpy(ctx->h_gather + off, pkts[i], lens[i]);
+        else d.len = 0xFFFF, d.offset = 0xFFFFFFFFu;   // -> BAD_DESC
+        off += ((uint64_t)lens[i] + 63) & ~63ull;
+    }
+    return mtcp_gpu_rx_chunk(ctx, ctx->h_gather, total, ctx->h_gather_desc, n, 6, out);
+}
+
+int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mtcp_gpu_desc *desc,
+                     uint32_t n, uint32_t off_shift, uint32_t *n_filled) {
+    if (!ctx || (n && (!buf || !desc)) || off_shift > 16) return MTCP_GPU_EINVAL;
+    if (n_filled) *n_filled = 0;
+    if (n == 0) return MTCP_GPU_OK;
+    (void)hipSetDevice(ctx->device);
+    Stage &s = ctx->stage[0];
+    const uint64_t cap = (buf_len + 15) & ~15ull;
+    int rc = stage_reserve(s, cap + 16, n);
+    if (rc != MTCP_GPU_OK) return rc;
+    if (!HIP_OK(hipMemsetAsync(s.d_buf + (buf_len & ~15ull), 0, 16, s.stream)) ||
+        !HIP_OK(hipMemcpyAsync(s.d_buf, buf, buf_len, hipMemcpyHostToDevice, s.stream)) ||
+        !HIP_OK(hipMemcpyAsync(s.d_desc, desc, (size_t)n * sizeof(mtcp_gpu_desc),
+                               hipMemcpyHostToDevice, s.stream)) ||
+        !HIP_OK(hipMemsetAsync(ctx->d_count, 0, sizeof(uint32_t), s.stream)))
+        return MTCP_GPU_EIO;
+    mg::KParams kp = base_params(ctx);
+    kp.buf = s.d_buf;
+    kp.buf_len = buf_len;   // descriptor bound: the caller's length
+    kp.desc = s.d_desc;
+    kp.n = n;
+    kp.off_shift = off_shift;
+    kp.fill_count = ctx->d_count;
+    rc = launch<mg::kTxChunk>(ctx, kp, s.stream);
+    uint32_t cnt = 0;
+    if (rc == MTCP_GPU_OK &&
+        (!HIP_OK(hipMemcpyAsync(buf, s.d_buf, buf_len, hipMemcpyDeviceToHost, s.stream)) ||
+         !HIP_OK(hipMemcpyAsync(&cnt, ctx->d_count, sizeof(cnt), hipMemcpyDeviceToHost, s.stream))))
+        rc = MTCP_GPU_EIO;
+    if (!HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK) rc = MTCP_GPU_EIO;
+    if (rc == MTCP_GPU_OK && n_filled) *n_filled = cnt;
+    return rc;
+}
+
+int mtcp_gpu_host_register(void *ptr, uint64_t len) {
+    if (!ptr || !len) return MTCP_GPU_EINVAL;
+    return HIP_OK(hipHostRegister(ptr, len, hipHostRegisterMapped)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
+}
+
+int mtcp_gpu_host_unregister(void *ptr) {
+    if (!ptr) return MTCP_GPU_EINVAL;
+    return HIP_OK(hipHostUnregister(ptr)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
+}
+
+}  // extern "C"

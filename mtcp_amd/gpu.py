@@ -1,0 +1,152 @@
+"""Python view of the C ABI (include/mtcp_gpu.h) for tests and bench.py.
+
+Device memory and streams come from PyTorch-ROCm (plumbing only); every
+computation runs in libmtcp_gpu.so's gfx950 kernels.  Mirrors the
+reference's operator boundary: `dev_ioctl` answers like
+io_module_func.dev_ioctl (mtcp/src/include/io_module.h:67, :80-87), rx calls
+return one verdict per packet in place of ProcessPacket's return value
+(mtcp/src/eth_in.c:9-56).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib
+from ._types import DESC_DTYPE, RESULT_DTYPE
+
+F_RSS = 0x1
+F_RSS_ENDIAN = 0x2
+
+PKT_TX_IP_CSUM = 0x01
+PKT_TX_TCP_CSUM = 0x02
+PKT_RX_TCP_LROSEG = 0x03
+PKT_TX_TCPIP_CSUM = 0x04
+PKT_RX_IP_CSUM = 0x05
+PKT_RX_TCP_CSUM = 0x06
+PKT_TX_TCPIP_CSUM_PEEK = 0x07
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream   # torch.cuda.Stream
+
+
+def _dptr(t) -> int:
+    if not t.is_cuda:
+        raise ValueError("device-resident entry points take GPU tensors")
+    return t.data_ptr()
+
+
+class Context:
+    """One mtcp_gpu_ctx (one per mTCP thread; not re-entrant)."""
+
+    def __init__(self, device: int = 0, rss: bool = False, rss_key: bytes | None = None,
+                 rss_queues: int = 1, rss_endian: bool = True):
+        L = lib()
+        self._h = ctypes.c_void_p()
+        flags = (F_RSS if rss else 0) | (F_RSS_ENDIAN if (rss and rss_endian) else 0)
+        key = None
+        if rss_key is not None:
+            if len(rss_key) != 40:
+                raise ValueError("RSS key must be 40 bytes (util/rss.c:84-90)")
+            self._key = (ctypes.c_uint8 * 40).from_buffer_copy(rss_key)
+            key = ctypes.cast(self._key, ctypes.c_void_p)
+        check(L.mtcp_gpu_open(ctypes.byref(self._h), device, key, rss_queues, flags),
+              "mtcp_gpu_open")
+        self.device = device
+
+    # -- lifetime ----------------------------------------------------------
+    def close(self) -> None:
+        if self._h:
+            lib().mtcp_gpu_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return lib().mtcp_gpu_stream(self._h) or 0
+
+    def sync(self) -> None:
+        check(lib().mtcp_gpu_sync(self._h), "mtcp_gpu_sync")
+
+    def dev_ioctl(self, cmd: int, nif: int = 0) -> int:
+        return lib().mtcp_gpu_dev_ioctl(self._h, nif, cmd, None)
+
+    # -- device-resident ---------------------------------------------------
+    def rx_chunk_dev(self, buf, desc, n: int, off_shift: int, out, stream=None) -> None:
+        check(lib().mtcp_gpu_rx_chunk_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
+                                          _dptr(desc), n, off_shift, _dptr(out),
+                                          _stream_handle(stream)), "mtcp_gpu_rx_chunk_dev")
+
+    def rx_ptrs_dev(self, ptrs, lens, n: int, out, stream=None) -> None:
+        check(lib().mtcp_gpu_rx_ptrs_dev(self._h, _dptr(ptrs), _dptr(lens), n, _dptr(out),
+                                         _stream_handle(stream)), "mtcp_gpu_rx_ptrs_dev")
+
+    def tx_fill_dev(self, buf, desc, n: int, off_shift: int, stream=None) -> None:
+        check(lib().mtcp_gpu_tx_fill_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
+                                         _dptr(desc), n, off_shift, _stream_handle(stream)),
+              "mtcp_gpu_tx_fill_dev")
+
+    # -- host memory ---------------------------------------------------------
+    def rx_chunk(self, buf: np.ndarray, desc: np.ndarray, off_shift: int = 0,
+                 out: np.ndarray | None = None) -> np.ndarray:
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        if out is None:
+            out = np.zeros(len(desc), dtype=RESULT_DTYPE)
+        check(lib().mtcp_gpu_rx_chunk(self._h, buf.ctypes.data, buf.nbytes, desc.ctypes.data,
+                                      len(desc), off_shift, out.ctypes.data), "mtcp_gpu_rx_chunk")
+        return out
+
+    def rx_ptrs(self, frames: list) -> np.ndarray:
+        n = len(frames)
+        arrs = [np.ascontiguousarray(np.frombuffer(bytes(f), dtype=np.uint8)) for f in frames]
+        ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        lens = np.array([a.nbytes for a in arrs], dtype=np.uint16)
+        out = np.zeros(n, dtype=RESULT_DTYPE)
+        check(lib().mtcp_gpu_rx_ptrs(self._h, ctypes.cast(ptrs, ctypes.c_void_p),
+                                     lens.ctypes.data, n, out.ctypes.data), "mtcp_gpu_rx_ptrs")
+        return out
+
+    def tx_fill(self, buf: np.ndarray, desc: np.ndarray, off_shift: int = 0) -> int:
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        cnt = ctypes.c_uint32(0)
+        check(lib().mtcp_gpu_tx_fill(self._h, buf.ctypes.data, buf.nbytes, desc.ctypes.data,
+                                     len(desc), off_shift, ctypes.byref(cnt)), "mtcp_gpu_tx_fill")
+        return cnt.value
+
+
+def host_register(arr: np.ndarray) -> None:
+    check(lib().mtcp_gpu_host_register(arr.ctypes.data, arr.nbytes), "mtcp_gpu_host_register")
+
+
+def host_unregister(arr: np.ndarray) -> None:
+    check(lib().mtcp_gpu_host_unregister(arr.ctypes.data), "mtcp_gpu_host_unregister")
+
+
+def pktgen_dev(buf, desc, n: int, off_shift: int, seed: int, first_index: int = 0,
+               stream=None) -> None:
+    """Synthetic frames on the GPU (include/mtcp_gpu_pktgen.h)."""
+    check(lib().mtcp_gpu_pktgen_dev(_dptr(buf), buf.numel() * buf.element_size(), _dptr(desc),
+                                    n, off_shift, seed, first_index, _stream_handle(stream)),
+          "mtcp_gpu_pktgen_dev")
+
+
+def results_view(t) -> np.ndarray:
+    """A device result buffer (uint8 tensor of n*40 bytes) as a numpy record array."""
+    return t.cpu().numpy().view(RESULT_DTYPE)

@@ -1,0 +1,150 @@
+"""The C oracle against the reference's golden vectors (CPU only).
+
+Pins oracle/mtcp_oracle.c — the parity checker for every GPU test — to the
+reference's own code: verdicts of the real ProcessPacket chain
+(mtcp/src/eth_in.c:9-56, ip_in.c:15-62, tcp_in.c:1138-1175), values of the
+real ip_fast_csum (io_engine/include/ps.h:66-95), TCPCalcChecksum
+(mtcp/src/tcp_util.c:157-190) and GetRSSHash / GetRSSCPUCore (util/rss.c,
+mtcp/src/rss.c), and the Microsoft Toeplitz KATs of util/rss.c:185-189.
+"""
+import socket
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+from tests.golden_io import compare_results
+
+V_TRUNCATED = 10
+
+
+def test_ip_fast_csum_vectors(golden):
+    c = golden.csum_ip
+    got = np.array([oracle.ip_fast_csum(bytes(c["hdr"][i]), int(c["ihl"][i]))
+                    for i in range(len(c))], dtype=np.uint16)
+    assert np.array_equal(got, c["csum"])
+    # ihl <= 4 returns the first dword unfolded (ps.h:72-73): covered above
+    assert (c["ihl"] <= 4).sum() >= 16
+
+
+def test_ip_fast_csum_worked_example():
+    # 45 00 00 73 00 00 40 00 40 11 [00 00] c0 a8 00 01 c0 a8 00 c7 -> b8 61
+    hdr = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
+    assert oracle.ip_fast_csum(hdr, 5) == 0x61b8
+    filled = hdr[:10] + struct.pack("<H", 0x61b8) + hdr[12:]
+    assert oracle.ip_fast_csum(filled, 5) == 0
+
+
+def test_tcp_checksum_vectors(golden):
+    c = golden.csum_tcp
+    for i in range(len(c)):
+        got = oracle.tcp_calc_checksum(bytes(c["seg"][i]), int(c["len"][i]),
+                                       int(c["saddr"][i]), int(c["daddr"][i]))
+        assert got == c["csum"][i], (i, int(c["len"][i]))
+
+
+def test_closed_form_fold():
+    """a2' of SURVEY §8: ~(S mod 0xFFFF, 0 -> 0xFFFF when S > 0) for ihl >= 5."""
+    rng = np.random.default_rng(7)
+    for _ in range(20000):
+        ihl = int(rng.integers(5, 16))
+        hdr = rng.integers(0, 256, size=4 * ihl, dtype=np.uint8)
+        if rng.random() < 0.05:
+            hdr[:] = 0xFF
+        words = hdr.view("<u2").astype(np.int64)
+        s = int(words.sum())
+        r = s % 0xFFFF
+        if r == 0 and s > 0:
+            r = 0xFFFF
+        assert oracle.ip_fast_csum(hdr.tobytes(), ihl) == (~r) & 0xFFFF
+
+
+def test_rss_microsoft_kat():
+    """util/rss.c:173-189 (VerifyRSSHash): host-order inputs, Microsoft key."""
+    src = ["66.9.149.187", "199.92.111.2", "24.19.198.95", "38.27.205.30", "153.39.163.191"]
+    dst = ["161.142.100.80", "65.69.140.83", "12.22.207.184", "209.142.163.6",
+           "202.188.127.2"]
+    sport = [2794, 14230, 12898, 48228, 44251]
+    dport = [1766, 4739, 38024, 2217, 1303]
+    want = [0x51ccc178, 0xc626b0ea, 0x5c2b394a, 0xafc7327f, 0x10e828a2]
+    cache = oracle.key_cache(oracle.KEY_MICROSOFT)
+    for s, d, sp, dp, w in zip(src, dst, sport, dport, want):
+        sip = struct.unpack("!I", socket.inet_aton(s))[0]
+        dip = struct.unpack("!I", socket.inet_aton(d))[0]
+        assert oracle.rss_hash(cache, sip, dip, sp, dp) == w
+
+
+def test_rss_vectors_0x05(golden):
+    r = golden.rss
+    cache = oracle.key_cache(oracle.KEY_0X05)
+    for i in range(len(r)):
+        args = (int(r["sip"][i]), int(r["dip"][i]), int(r["sp"][i]), int(r["dp"][i]))
+        assert oracle.rss_hash(cache, *args) == r["hash"][i]
+        for nq in (1, 2, 3, 4, 7, 8, 16):
+            assert oracle.rss_cpu_core(cache, *args, nq, 1) == r["util_core"][i][nq - 1]
+            assert oracle.rss_cpu_core(cache, *args, nq, 0) == r["mtcp_core0"][i][nq - 1]
+            assert oracle.rss_cpu_core(cache, *args, nq, 1) == r["mtcp_core1"][i][nq - 1]
+
+
+def test_rx_chunk_matches_reference(golden):
+    rss = oracle.rss_cfg(oracle.KEY_0X05, golden.rss_num_queues, 1)
+    got = oracle.rx_chunk(golden.buf, golden.desc, 0, rss)
+    bad = compare_results(got, golden)
+    assert not bad, bad
+    # TRUNCATED exactly where the reference would read past len
+    assert np.array_equal(got["verdict"] == V_TRUNCATED, golden.meta["ref_ub"] == 1)
+    # every branch of the chain is covered by the fixtures
+    branches = set(golden.meta["branch"][golden.meta["ref_ub"] == 0].tolist())
+    assert branches == set(range(10))
+
+
+def test_rx_verdicts_match_reference_return_values(golden):
+    """ProcessPacket's return (ERROR -1 / FALSE 0 / TRUE 1) against the verdict."""
+    ok = golden.meta["ref_ub"] == 0
+    ret = golden.meta["ret"].astype(np.int32) - 1
+    v = golden.expect["verdict"]
+    err = np.isin(v, [3, 4, 8, 9])
+    assert np.all(ret[ok & err] == -1)
+    assert np.all(ret[ok & np.isin(v, [5, 7])] == 0)
+    assert np.all(ret[ok & np.isin(v, [1, 2, 6])] == 1)
+    # the reference zeroes tcph->check on a bad TCP checksum (tcp_in.c:1171)
+    assert golden.meta["check_zeroed"][ok & (v == 9)].sum() >= (ok & (v == 9)).sum() - 1
+
+
+def test_tx_fill_matches_reference(golden):
+    buf = golden.buf.copy()
+    n = oracle.tx_fill(buf, golden.desc, 0)
+    assert n == golden.manifest["tx_filled"]
+    tx = golden.tx
+    for i in np.nonzero(tx["filled"])[0]:
+        off = int(golden.desc["offset"][i])
+        t = int(tx["T"][i])
+        assert buf[off + 24:off + 26].view("<u2")[0] == tx["ip_check"][i]
+        assert buf[off + t + 16:off + t + 18].view("<u2")[0] == tx["tcp_check"][i]
+
+
+def test_pktgen_samples_match_fixture(golden):
+    """The oracle's generator reproduces the sample bytes stored in the fixture."""
+    for s in golden.manifest["samples"]:
+        first, count = s["first"], s["count"]
+        d = golden.desc[first:first + count].copy()
+        base = int(d["offset"][0])
+        end = int(d["offset"][-1]) + ((int(d["len"][-1]) + 63) & ~63)
+        d["offset"] -= base
+        buf = np.zeros(end - base, np.uint8)
+        oracle.pktgen(buf, d, 0, s["seed"], 0)
+        assert np.array_equal(buf, golden.buf[base:end]), s["name"]
+
+
+def test_pktgen_corruption_rates():
+    from mtcp_amd import pktgen
+    n = 1 << 16
+    desc, size = pktgen.layout(n, 1500, off_shift=6)
+    buf = np.zeros(size, np.uint8)
+    oracle.pktgen(buf, desc, 6, 2, 0)
+    res = oracle.rx_chunk(buf, desc, 6)
+    counts = np.bincount(res["verdict"], minlength=12)
+    assert counts[0] > n * 0.99
+    assert 20 < counts[9] < 120            # ~1/1024 TCP bit flips
+    assert 3 < counts[4] < 40              # ~1/4096 IP header bit flips

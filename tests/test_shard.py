@@ -1,0 +1,71 @@
+"""Batch split across ranks, checked on CPU with the oracle:
+world_size-2 gloo processes each process their shard; the gathered results
+equal the single-batch results packet for packet."""
+import os
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from mtcp_amd import pktgen, shard
+
+
+def _full(n, size, seed):
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    return buf, desc
+
+
+@pytest.mark.parametrize("size", [1500, "bimodal"])
+def test_bounds_balance(size):
+    b = shard.bounds(10000, size, 4, seed=3)
+    assert b[0] == 0 and b[-1] == 10000 and all(x <= y for x, y in zip(b, b[1:]))
+    if size == "bimodal":
+        lens = pktgen.lengths(10000, size, 3)
+        padded = (lens.astype(np.int64) + 63) & ~63
+        per = [padded[b[r]:b[r + 1]].sum() for r in range(4)]
+        assert max(per) - min(per) <= 2 * 1536
+
+
+def _worker(rank, world, port, size, n, seed, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = shard.make_shard(n, size, rank, world, seed)
+    buf = np.zeros(s.nbytes, np.uint8)
+    oracle.pktgen(buf, s.desc, 6, seed, s.first_index)
+    res = oracle.rx_chunk(buf, s.desc, 6, oracle.rss_cfg(None, 4, 1))
+    import torch
+    t = torch.from_numpy(res.view(np.uint8).copy())
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([t.numel()]))
+    mx = int(max(x.item() for x in sizes))
+    pad = torch.zeros(mx, dtype=torch.uint8)
+    pad[:t.numel()] = t
+    gathered = [torch.zeros(mx, dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(gathered, pad)
+    if rank == 0:
+        out = b"".join(g[:int(sz.item())].numpy().tobytes() for g, sz in zip(gathered, sizes))
+        q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size", [1500, "bimodal"])
+def test_two_rank_shards_equal_full_batch(size):
+    n, seed = 3000, 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, size, n, seed, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    buf, desc = _full(n, size, seed)
+    want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(None, 4, 1))
+    assert got == want.tobytes()
