@@ -55,7 +55,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
-    ap.add_argument("--cpu-sample", type=int, default=1 << 17, help="packets in the CPU sample")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 20,
+                    help="packets in the CPU sample (default: the whole 1-GPU batch, "
+                         "larger than the host L3, so the CPU streams from DRAM like the GPU)")
     ap.add_argument("--pcie", default="auto", choices=["auto", "on", "off"])
     return ap.parse_args()
 
@@ -151,7 +153,9 @@ def main():
     n_total = cfg["per_gpu"] * world
     sh = shard.make_shard(n_total, cfg["size"], rank, world, cfg["seed"])
     dev = torch.device("cuda", local_rank)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: the kernel and the timing events share it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     d_buf = torch.empty(sh.nbytes, dtype=torch.uint8, device=dev)
     d_desc = torch.from_numpy(sh.desc.view(np.uint8).copy()).to(dev)
     d_out = torch.empty(sh.count * 40, dtype=torch.uint8, device=dev)
