@@ -9,7 +9,7 @@ LIB      := mtcp_amd/lib/libmtcp_gpu.so
 SRCS     := mtcp_amd/csrc/mtcp_gpu.hip mtcp_amd/csrc/pktgen.hip
 DEPS     := $(SRCS) mtcp_amd/csrc/rx_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h
 
-.PHONY: all lib oracle ref golden examples clean
+.PHONY: all lib oracle ref golden examples clean tools
 
 all: lib oracle
 
@@ -31,3 +31,11 @@ golden:
 clean:
 	rm -f $(LIB)
 	$(MAKE) -C oracle clean
+
+tools/rx_variants: tools/rx_variants.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
+
+tools/hbm_ceiling: tools/hbm_ceiling.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -w -o $@ $<
+
+tools: tools/rx_variants tools/hbm_ceiling

@@ -53,8 +53,9 @@ namespace {
 
 #define HIP_OK(x) ((x) == hipSuccess)
 
-// util/rss.c:13-105 (BuildKeyCache), then the 12 byte tables the kernel XORs:
-// table[t][v] = XOR of cache[8t + m] over the bits of v, MSB first.
+// util/rss.c:13-105 (BuildKeyCache), then the 24 nibble tables the kernel
+// XORs: table[t][v] = XOR of cache[4t + m] over the bits of nibble v, MSB
+// first (nibble t of the 96-bit input sip|dip|sp|dp, most significant first).
 void build_rss_tables(const uint8_t key[40], uint32_t *tables) {
     uint32_t cache[96];
     uint32_t result = ((uint32_t)key[0] << 24) | ((uint32_t)key[1] << 16) |
@@ -65,12 +66,12 @@ void build_rss_tables(const uint8_t key[40], uint32_t *tables) {
         const uint32_t bit = ((key[idx / 8] << (idx % 8)) & 0x80) ? 1u : 0u;
         result = (result << 1) | bit;
     }
-    for (int t = 0; t < 12; ++t)
-        for (int v = 0; v < 256; ++v) {
+    for (int t = 0; t < 24; ++t)
+        for (int v = 0; v < 16; ++v) {
             uint32_t h = 0;
-            for (int m = 0; m < 8; ++m)
-                if (v & (0x80 >> m)) h ^= cache[8 * t + m];
-            tables[t * 256 + v] = h;
+            for (int m = 0; m < 4; ++m)
+                if (v & (0x8 >> m)) h ^= cache[4 * t + m];
+            tables[t * 16 + v] = h;
         }
 }
 

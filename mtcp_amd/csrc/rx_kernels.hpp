@@ -5,25 +5,29 @@
 // (mtcp/src/tcp_util.c:157-190), the Toeplitz RSS hash (util/rss.c:107-165),
 // and the tx checksum fill (ip_out.c:94,164; tcp_out.c:211,329).
 //
-// Work decomposition (one 64-lane wave per group of 64 packets):
-//   phase 0  lane k parses packet k of the group: descriptor, the header
-//            dwords it needs (L1/L2-resident gathers), verdict up to the TCP
-//            checksum, and the TCP segment [T, 14+tot_len) as a range of
-//            16-byte aligned chunks.
-//   phase 1  the WHOLE wave streams each packet's chunks in turn, 1 KiB per
-//            wave-instruction (global_load_dwordx4, lane l -> chunk l), adds
-//            the 16-bit halves with v_sad_u16 and reduces across the wave
-//            with DPP; two packets are in flight at once.
-//   phase 2  lane k removes the bytes the aligned chunks over-cover (the
-//            <= 14 header bytes before T and the <= 15 bytes after the
-//            segment), adds the pseudo header, folds, finishes the verdict,
-//            hashes the 4-tuple through 12 byte tables in LDS, and stores its
-//            40-byte record.
-// Exactness: the reference sums little-endian u16 words of the segment into
-// a u32 (no overflow for any u16 length).  The segment starts at an even
-// address, so its words are exactly the 16-bit halves of the aligned dwords
-// that hold it; every partial sum here is an exact integer below 2^31 and
-// the final fold is the reference's own two-step fold.
+// Work decomposition: one 64-lane wave per group of 64 consecutive packets;
+// lane k owns packet k of the group.
+//   phase 0  lane k loads its descriptor (one coalesced 8-byte load); no
+//            header is read yet.
+//   phase 1  the four 16-lane DPP rows of the wave stream four frames at a
+//            time (round i: row r takes frame 4i + r), each row 256 B per
+//            wave-instruction on the absolute 16 B chunk grid, six loads
+//            (6 KiB per wave) issued before any is consumed — a 1500 B frame
+//            is one round trip.  v_sad_u16 adds the 16-bit halves; a row
+//            reduction (4 DPP row_shr adds) leaves each frame's chunk sum in
+//            LDS.  While a frame is in registers its first seven chunks (the
+//            headers) and its last chunk are copied to the owner's LDS slot.
+//   phase 2  lane k parses its headers from LDS (verdict chain, fields, IP
+//            checksum), subtracts from the chunk sum the bytes outside the
+//            TCP segment [T, E) (E = 14 + tot_len), adds the pseudo header,
+//            folds, hashes the 4-tuple through 24 nibble tables in LDS and
+//            stores its record (staged in LDS, written as whole 16 B lanes).
+// HBM traffic is one pass over the frames plus descriptors and results.
+// Exactness: the reference sums little-endian u16 words into a u32 (no
+// overflow for any u16 length).  Every packet starts at an even address, so
+// its words are exactly the 16-bit halves of the aligned dwords that hold
+// it; all partial sums here are exact integers below 2^31 and the final fold
+// is the reference's own two-step fold.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -36,13 +40,16 @@ namespace mg {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kRssTableWords = 12 * 256;
+constexpr int kRssTableWords = 24 * 16;  // nibble tables
+constexpr int kSlotChunks = 8;           // chunks 0..6 raw (headers), 7 = last chunk
+constexpr int kRow = 16;                 // lanes per DPP row = lanes per frame
+constexpr int kUnroll = 6;               // loads in flight per row (96 chunks = 1536 B)
 
 enum Mode : int { kRxChunk = 0, kRxPtrs = 1, kTxChunk = 2 };
 
 struct KParams {
-    const uint8_t *buf;            // chunk base (chunk modes)
-    uint64_t buf_len;              // readable bytes from buf (multiple of 16)
+    const uint8_t *buf;            // chunk base (chunk modes), 16 B aligned
+    uint64_t buf_len;              // descriptor bound: bytes valid from buf
     int64_t base_sub;              // subtracted from every descriptor byte offset
     const mtcp_gpu_desc *desc;
     const uint8_t *const *ptrs;    // pointer mode
@@ -50,11 +57,13 @@ struct KParams {
     uint32_t n;
     uint32_t off_shift;
     mtcp_gpu_result *out;
-    const uint32_t *rss_tables;    // 12 x 256 Toeplitz byte tables
+    const uint32_t *rss_tables;    // 24 x 16 Toeplitz nibble tables
     uint32_t rss_nq;
     uint32_t rss_endian;
     uint32_t *fill_count;          // tx fill: frames written (may be null)
 };
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t v) {
     return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu);
@@ -65,7 +74,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap
 __device__ __forceinline__ uint32_t halves(uint32_t d, uint32_t acc) {
     return __builtin_amdgcn_sad_u16(d, 0u, acc);
 }
-__device__ __forceinline__ uint32_t halves4(const uint4 &v, uint32_t acc) {
+__device__ __forceinline__ uint32_t halves4(const v4u &v, uint32_t acc) {
     return halves(v.w, halves(v.z, halves(v.y, halves(v.x, acc))));
 }
 
@@ -77,91 +86,120 @@ __device__ __forceinline__ uint32_t fold_csum(uint32_t s) {
     return (~s) & 0xFFFFu;
 }
 
-// Wave-wide u32 sum via DPP; the total is returned in every lane (SGPR).
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+// Sum over each 16-lane row; the row total lands in the row's lane 15.
+__device__ __forceinline__ uint32_t row_sum(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return v;
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
-    uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
-    uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
-    return ((uint64_t)hi << 32) | lo;
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 
-// Sum of the halves of chunk windows [w0, ...) of one packet (jumbo tail).
-__device__ __forceinline__ uint32_t sum_rest(const uint4 *base, uint32_t nch, uint32_t lane) {
-    uint32_t acc = 0;
-    for (uint32_t c0 = 2 * kWave; c0 < nch; c0 += 4 * kWave) {
-        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0, v3 = v0;
-        uint32_t c = c0 + lane;
-        if (c < nch) v0 = base[c];
-        if (c + kWave < nch) v1 = base[c + kWave];
-        if (c + 2 * kWave < nch) v2 = base[c + 2 * kWave];
-        if (c + 3 * kWave < nch) v3 = base[c + 3 * kWave];
-        acc = halves4(v0, acc);
-        acc = halves4(v1, acc);
-        acc = halves4(v2, acc);
-        acc = halves4(v3, acc);
-    }
-    return acc;
-}
+// Per-wave LDS: one 128 B slot per packet (raw chunks 0..6 of the frame on
+// the 16 B grid, then its last chunk) and the per-frame chunk sums.
+struct WaveLds {
+    uint4 slot[kWave][kSlotChunks];
+    uint32_t sum[kWave];
+};
 
 template <int MODE, bool RSS>
 __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
+    __shared__ WaveLds lds[kWavesPerBlock];
     if constexpr (RSS) {
         for (int i = threadIdx.x; i < kRssTableWords; i += kBlock) rss_lds[i] = kp.rss_tables[i];
         __syncthreads();
     }
 
     const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint32_t row = lane >> 4, rlane = lane & (kRow - 1);
+    const uint32_t wib = threadIdx.x >> 6;
+    const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
     const uint32_t ngroups = (kp.n + kWave - 1) / kWave;
+    WaveLds &wl = lds[wib];
 
     for (uint32_t g = wave; g < ngroups; g += nwaves) {
         const uint32_t k = g * kWave + lane;
         const bool live = k < kp.n;
 
-        // ---------------- phase 0: per-lane parse -------------------------
-        const uint8_t *pkt = nullptr;
+        // ---------------- phase 0: descriptor -----------------------------
+        uint64_t p = (uint64_t)(uintptr_t)(MODE == kRxPtrs ? (const void *)kp.out : (const void *)kp.buf);
         uint32_t L = 0;
         bool desc_ok = false;
         if (live) {
             if constexpr (MODE == kRxPtrs) {
-                pkt = kp.ptrs[k];
+                p = (uint64_t)(uintptr_t)kp.ptrs[k];
                 L = kp.lens[k];
-                desc_ok = pkt != nullptr && (((uintptr_t)pkt) & 3) == 0;
+                desc_ok = p != 0 && (p & 3) == 0;
+                // rows with nothing to read still issue (clamped) loads: give
+                // them an address that is always mapped
+                if (!desc_ok) p = (uint64_t)(uintptr_t)kp.out;
             } else {
                 const mtcp_gpu_desc d = kp.desc[k];
                 const int64_t pos = (int64_t)((uint64_t)d.offset << kp.off_shift) - kp.base_sub;
                 L = d.len;
                 desc_ok = pos >= 0 && (pos & 3) == 0 && (uint64_t)pos + L <= kp.buf_len;
-                pkt = kp.buf + (desc_ok ? pos : 0);
+                p += (uint64_t)(desc_ok ? pos : 0);
             }
         }
-        const uint32_t *pw = reinterpret_cast<const uint32_t *>(pkt);
-        // header dword at byte offset o (o % 4 == 0): only bytes < L are read
-        auto ldw = [&](uint32_t o) -> uint32_t { return (desc_ok && o < L) ? pw[o >> 2] : 0u; };
+        // chunk range of the frame on the 16 B grid: [p16, p16 + 16*nch)
+        const uint64_t p16 = p & ~15ull;
+        const uint32_t nch = desc_ok && L ? (uint32_t)((((p + L + 15) & ~15ull) - p16) >> 4) : 0u;
+
+        // ---------------- phase 1: four frames per wave-instruction ---------
+        if (__ballot(nch != 0)) {
+            for (int i = 0; i < kWave / 4; ++i) {
+                const int j = 4 * i + (int)row;                    // this row's frame
+                const uint32_t nj = shfl32(nch, j);
+                if (!__ballot(nj != 0)) continue;
+                const uint64_t bj = ((uint64_t)shfl32((uint32_t)(p16 >> 32), j) << 32) |
+                                    shfl32((uint32_t)p16, j);
+                const uint4 *base = reinterpret_cast<const uint4 *>(bj);
+                uint32_t acc = 0;
+                for (uint32_t c0 = 0;; c0 += kUnroll * kRow) {
+                    v4u x[kUnroll];
+#pragma unroll
+                    for (int u = 0; u < kUnroll; ++u) {
+                        const uint32_t c = c0 + u * kRow + rlane;
+                        const uint32_t cc = c < nj ? c : (nj ? nj - 1 : 0u);   // clamp: no exec mask
+                        x[u] = *reinterpret_cast<const v4u *>(base + cc);
+                    }
+                    if (c0 == 0 && rlane < kSlotChunks - 1)              // raw chunks 0..6
+                        wl.slot[j][rlane] = make_uint4(x[0].x, x[0].y, x[0].z, x[0].w);
+#pragma unroll
+                    for (int u = 0; u < kUnroll; ++u) {
+                        const uint32_t c = c0 + u * kRow + rlane;
+                        const uint32_t s = halves4(x[u], 0u);
+                        acc += c < nj ? s : 0u;
+                        if (c == nj - 1) wl.slot[j][kSlotChunks - 1] = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
+                    }
+                    if (!__ballot(c0 + kUnroll * kRow < nj)) break;
+                }
+                acc = row_sum(acc);
+                if (rlane == kRow - 1) wl.sum[j] = acc;
+            }
+        }
+
+        // ---------------- phase 2: per-lane parse and finish ---------------
+        const uint32_t sh = (uint32_t)(p & 15);
+        const uint32_t *raw = reinterpret_cast<const uint32_t *>(wl.slot[lane]);
+        const uint32_t *hw = raw + (sh >> 2);      // packet dword i at hw[i]
+        uint32_t h[24];
+#pragma unroll
+        for (int i = 0; i < 24; ++i) h[i] = hw[i];
 
         uint32_t verdict = MTCP_GPU_V_BAD_DESC;
         uint32_t eth_type = 0, ip_len = 0, ihl = 0, ihl_doff = 0, ip_csum = 0;
         uint32_t saddr = 0, daddr = 0, ports = 0, seq = 0, ack = 0, window = 0, flags = 0;
         uint32_t payload_len = 0, rss_hash = 0, rss_queue = 0;
-        bool need_sum = false;   // TCP segment checksum pending
-        uint32_t tcp_len = 0, T = 0, s_ip = 0, d0 = 0, d3 = 0, s_head = 0, tcheck = 0;
-
-        uint32_t d[16];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) d[j] = ldw(12 + 4 * j);
-        d0 = d[0];
-        d3 = d[3];
+        uint32_t tcp_len = 0, T = 0, s_ip = 0, tcheck = 0, tcp_csum = 0;
+        bool need_sum = false;
+        const uint32_t d0 = h[3];                 // bytes 12..15
         if (desc_ok) {
             verdict = MTCP_GPU_V_TRUNCATED;
             if (L >= 14) {
@@ -169,26 +207,24 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 if (eth_type != 0x0800u) {
                     verdict = eth_type == 0x0806u ? MTCP_GPU_V_ARP : MTCP_GPU_V_ETH_OTHER;
                 } else if (L >= 18) {
-                    ip_len = bswap16(d[1] & 0xFFFFu);                      // ip_in.c:21
+                    ip_len = bswap16(h[4] & 0xFFFFu);                      // ip_in.c:21
                     ihl = (d0 >> 16) & 0xFu;
                     ihl_doff = ihl;
                     const uint32_t ver = (d0 >> 20) & 0xFu;
                     if (MODE != kTxChunk && ip_len < 20) {
                         verdict = MTCP_GPU_V_IP_SHORT;                     // ip_in.c:25-26
                     } else if (L >= 14 + 4 * (ihl > 1 ? ihl : 1)) {
-#pragma unroll
-                        for (int j = 6; j < 16; ++j) d[j] = (j <= (int)ihl) ? ldw(12 + 4 * j) : 0u;
                         // ip_fast_csum: ihl <= 4 returns dword 0 as is (ps.h:72-73)
                         s_ip = d0 >> 16;
                         uint32_t lo_last = 0;
 #pragma unroll
                         for (int j = 1; j < 16; ++j) {
-                            if (j < (int)ihl) s_ip = halves(d[j], s_ip);
-                            if (j == (int)ihl) lo_last = d[j] & 0xFFFFu;
+                            if (j < (int)ihl) s_ip = halves(h[3 + j], s_ip);
+                            if (j == (int)ihl) lo_last = h[3 + j] & 0xFFFFu;
                         }
                         s_ip += lo_last;
                         ip_csum = ihl <= 4 ? (d0 >> 16) : fold_csum(s_ip);
-                        const uint32_t proto = d[2] >> 24;                 // ip_in.c:52
+                        const uint32_t proto = h[5] >> 24;                 // ip_in.c:52
                         T = 14 + 4 * ihl;
                         bool tcp_entry = false;
                         if (MODE == kTxChunk) {
@@ -207,11 +243,12 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                         }
                         if (tcp_entry) {
                             // tcp_in.c:1142-1149: tcph = iph + 4*ihl
-                            const uint32_t e0 = ldw(T - 2), e1 = ldw(T + 2), e2 = ldw(T + 6);
-                            const uint32_t e3 = ldw(T + 10), e4 = ldw(T + 14);
+                            const uint32_t tw = (T - 2) >> 2;
+                            const uint32_t e0 = hw[tw], e1 = hw[tw + 1], e2 = hw[tw + 2];
+                            const uint32_t e3 = hw[tw + 3], e4 = hw[tw + 4];
                             const uint32_t doff = (e3 >> 20) & 0xFu;
-                            saddr = (d[3] >> 16) | (d[4] << 16);
-                            daddr = (d[4] >> 16) | (d[5] << 16);
+                            saddr = (h[6] >> 16) | (h[7] << 16);
+                            daddr = (h[7] >> 16) | (h[8] << 16);
                             ports = (e0 >> 16) | (e1 << 16);               // sport | dport << 16
                             seq = bswap32((e1 >> 16) | (e2 << 16));
                             ack = bswap32((e2 >> 16) | (e3 << 16));
@@ -220,19 +257,25 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                             tcheck = e4 >> 16;
                             ihl_doff = ihl | (doff << 4);
                             if constexpr (RSS) {
-                                // util/rss.c:107-145 as 12 byte tables: the input
+                                // util/rss.c:107-145 as 24 nibble tables: the input
                                 // bytes (sip, dip, sp, dp host order, MSB first)
                                 // are saddr/daddr/ports in memory order.
-                                uint32_t h = 0;
+                                uint32_t hh = 0;
 #pragma unroll
                                 for (int b = 0; b < 4; ++b) {
-                                    h ^= rss_lds[(b << 8) | ((saddr >> (8 * b)) & 0xFFu)];
-                                    h ^= rss_lds[((4 + b) << 8) | ((daddr >> (8 * b)) & 0xFFu)];
-                                    h ^= rss_lds[((8 + b) << 8) | ((ports >> (8 * b)) & 0xFFu)];
+                                    const uint32_t sb = (saddr >> (8 * b)) & 0xFFu;
+                                    const uint32_t db = (daddr >> (8 * b)) & 0xFFu;
+                                    const uint32_t pb = (ports >> (8 * b)) & 0xFFu;
+                                    hh ^= rss_lds[((2 * b) << 4) | (sb >> 4)] ^
+                                          rss_lds[((2 * b + 1) << 4) | (sb & 15)];
+                                    hh ^= rss_lds[((8 + 2 * b) << 4) | (db >> 4)] ^
+                                          rss_lds[((9 + 2 * b) << 4) | (db & 15)];
+                                    hh ^= rss_lds[((16 + 2 * b) << 4) | (pb >> 4)] ^
+                                          rss_lds[((17 + 2 * b) << 4) | (pb & 15)];
                                 }
-                                rss_hash = h;
+                                rss_hash = hh;
                                 // util/rss.c:153-165: off[m & 3] = {3,1,-1,-3} == m ^ 3
-                                uint32_t m = h & 0x7Fu;
+                                uint32_t m = hh & 0x7Fu;
                                 if (kp.rss_endian) m ^= 3u;
                                 rss_queue = m % kp.rss_nq;
                             }
@@ -250,78 +293,50 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                                     tcp_len = ip_len - 4 * ihl;              // tcp_in.c:1166
                                 }
                             }
-                            if (need_sum) {
-                                // header bytes [s16, pkt+T) the first chunk over-covers
-                                const uint32_t hs = (uint32_t)(((uintptr_t)pkt + T) & 15u);
-                                const uint32_t hstart = T - hs;
-                                uint32_t sh = 0, lo2 = 0;
-#pragma unroll
-                                for (int j = 1; j < 16; ++j) {
-                                    if (j < (int)ihl && 12 + 4 * j >= (int)hstart) sh = halves(d[j], sh);
-                                    if (j == (int)ihl) lo2 = d[j] & 0xFFFFu;
-                                }
-                                s_head = sh + lo2;
-                            }
                         }
                     }
                 }
             }
         }
 
-        // chunk range of the TCP segment [pkt+T, pkt+14+ip_len)
-        uint64_t s16 = 0;
-        uint32_t nch = 0;
         if (need_sum) {
-            const uint64_t s = (uint64_t)(uintptr_t)pkt + T;
-            const uint64_t e = (uint64_t)(uintptr_t)pkt + 14 + ip_len;
-            s16 = s & ~15ull;
-            nch = (uint32_t)((((e + 15) & ~15ull) - s16) >> 4);
-        }
-
-        // ---------------- phase 1: wave-wide segment sums -----------------
-        uint32_t s_chunks = 0;
-        const uint64_t any = __ballot(nch != 0);
-        if (any) {
-            for (int j = 0; j < kWave; j += 2) {
-                if (((any >> j) & 3ull) == 0) continue;
-                const uint4 *ba = reinterpret_cast<const uint4 *>(readlane64(s16, j));
-                const uint4 *bb = reinterpret_cast<const uint4 *>(readlane64(s16, j + 1));
-                const uint32_t na = (uint32_t)__builtin_amdgcn_readlane((int)nch, j);
-                const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)nch, j + 1);
-                uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, b0 = a0, b1 = a0;
-                if (lane < na) a0 = ba[lane];
-                if (lane + kWave < na) a1 = ba[lane + kWave];
-                if (lane < nb) b0 = bb[lane];
-                if (lane + kWave < nb) b1 = bb[lane + kWave];
-                uint32_t acc_a = halves4(a1, halves4(a0, 0u));
-                uint32_t acc_b = halves4(b1, halves4(b0, 0u));
-                if (na > 2 * kWave) acc_a += sum_rest(ba, na, lane);
-                if (nb > 2 * kWave) acc_b += sum_rest(bb, nb, lane);
-                const uint32_t ta = wave_sum(acc_a);
-                const uint32_t tb = wave_sum(acc_b);
-                if (lane == (uint32_t)j) s_chunks = ta;
-                if (lane == (uint32_t)j + 1) s_chunks = tb;
+            // The chunk sum covers [p16, p16 + 16*nch).  Remove the bytes before
+            // the frame, the header bytes [0, T), and everything at or past
+            // E = 14 + ip_len.
+            uint32_t s_out = 0;
+            // (a) raw dwords before the frame (sh/4 of them) and header dwords
+            //     0 .. (T-2)/4 - 1, plus the low half of dword (T-2)/4
+            const int pre = (int)(sh >> 2);
+            const int tw = pre + (int)((T - 2) >> 2);
+#pragma unroll
+            for (int i = 0; i < 28; ++i) {
+                if (i < tw) s_out = halves(raw[i], s_out);
             }
-        }
-
-        // ---------------- phase 2: finish per lane ------------------------
-        uint32_t tcp_csum = 0;
-        if (need_sum) {
-            // bytes after the segment inside its last aligned chunk
-            const uint64_t e = (uint64_t)(uintptr_t)pkt + 14 + ip_len;
-            const uint32_t te = (uint32_t)(e & 15u);
-            uint32_t s_tail = 0;
+            s_out += raw[tw] & 0xFFFFu;
+            // (b) bytes [p + E, p16 + 16*nch)
+            const uint64_t e_abs = p + 14 + ip_len;
+            const uint64_t end = p16 + 16ull * nch;
+            const uint32_t te = (uint32_t)(e_abs & 15);
+            uint64_t cstart = e_abs & ~15ull;                      // chunk holding byte E
             if (te) {
-                const uint4 w = *reinterpret_cast<const uint4 *>(e & ~15ull);
+                // partial chunk: the last chunk when E and the frame end share it
+                uint4 w;
+                if (cstart + 16 == end) w = wl.slot[lane][kSlotChunks - 1];
+                else w = *reinterpret_cast<const uint4 *>(cstart);  // rare: E well before len
                 const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int drop = (int)te - 4 * i;   // low bytes inside the segment
                     const uint32_t m = drop <= 0 ? 0xFFFFFFFFu : drop >= 4 ? 0u : (0xFFFFFFFFu << (8 * drop));
-                    s_tail = halves(wv[i] & m, s_tail);
+                    s_out = halves(wv[i] & m, s_out);
                 }
+                cstart += 16;
             }
-            uint32_t s = s_chunks - s_head - s_tail;               // exact segment sum
+            for (; cstart < end; cstart += 16) {                   // rare: whole chunks past E
+                const uint4 w = *reinterpret_cast<const uint4 *>(cstart);
+                s_out = halves(w.w, halves(w.z, halves(w.y, halves(w.x, s_out))));
+            }
+            uint32_t s = wl.sum[lane] - s_out;                     // exact segment sum
             if (MODE == kTxChunk) s -= tcheck;                     // computed with check = 0
             s += (saddr & 0xFFFFu) + (saddr >> 16);                // tcp_util.c:179-182
             s += (daddr & 0xFFFFu) + (daddr >> 16);
@@ -332,23 +347,37 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 verdict = tcp_csum ? MTCP_GPU_V_TCP_CSUM_BAD : MTCP_GPU_V_TCP_OK;   // tcp_in.c:1167-1173
         }
 
-        if (!live) continue;
         if constexpr (MODE == kTxChunk) {
-            if (need_sum) {
-                const uint32_t ipc = fold_csum(s_ip - (d3 & 0xFFFFu));   // ip_out.c:145,164
-                uint16_t *p16 = reinterpret_cast<uint16_t *>(const_cast<uint8_t *>(pkt));
-                p16[12] = (uint16_t)ipc;                              // iph->check (byte 24)
-                p16[(T + 16) >> 1] = (uint16_t)tcp_csum;              // tcph->check (tcp_out.c:329)
+            if (live && need_sum) {
+                const uint32_t ipc = fold_csum(s_ip - (h[6] & 0xFFFFu));   // ip_out.c:145,164
+                uint16_t *q16 = reinterpret_cast<uint16_t *>(p);
+                q16[12] = (uint16_t)ipc;                              // iph->check (byte 24)
+                q16[(T + 16) >> 1] = (uint16_t)tcp_csum;              // tcph->check (tcp_out.c:329)
                 if (kp.fill_count) atomicAdd(kp.fill_count, 1u);
             }
         } else {
-            uint2 *o = reinterpret_cast<uint2 *>(kp.out + k);
-            o[0] = make_uint2(saddr, daddr);
-            o[1] = make_uint2(ports, seq);
-            o[2] = make_uint2(ack, window | (ip_len << 16));
-            o[3] = make_uint2(ip_csum | (tcp_csum << 16), rss_hash);
-            o[4] = make_uint2(payload_len | (ihl_doff << 16) | (flags << 24),
-                              verdict | (rss_queue << 8) | (eth_type << 16));
+            // stage the 64 records (2560 B) in this wave's LDS slots, then
+            // store them with full 16-byte lanes: 2.5 coalesced wave-stores
+            uint2 *st = reinterpret_cast<uint2 *>(wl.slot) + lane * 5;
+            st[0] = make_uint2(saddr, daddr);
+            st[1] = make_uint2(ports, seq);
+            st[2] = make_uint2(ack, window | (ip_len << 16));
+            st[3] = make_uint2(ip_csum | (tcp_csum << 16), rss_hash);
+            st[4] = make_uint2(payload_len | (ihl_doff << 16) | (flags << 24),
+                               verdict | (rss_queue << 8) | (eth_type << 16));
+            const uint32_t nrec = min((uint32_t)kWave, kp.n - g * kWave);
+            const uint4 *src = reinterpret_cast<const uint4 *>(wl.slot);
+            uint4 *dst = reinterpret_cast<uint4 *>(kp.out + (size_t)g * kWave);
+            const uint32_t n16 = nrec * 40 / 16;     // nrec * 40 is a multiple of 8
+#pragma unroll
+            for (uint32_t i = 0; i < 3; ++i) {
+                const uint32_t q = i * kWave + lane;
+                if (q < n16) dst[q] = src[q];
+            }
+            if ((nrec * 40) & 8) {                   // odd record count: last 8 bytes
+                if (lane == 0)
+                    reinterpret_cast<uint2 *>(dst)[n16 * 2] = reinterpret_cast<const uint2 *>(src)[n16 * 2];
+            }
         }
     }
 }
