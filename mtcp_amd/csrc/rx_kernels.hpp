@@ -65,6 +65,16 @@ struct KParams {
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
+// Loads through address-space-1 (global) pointers: a generic pointer built
+// from shuffled lane values would compile to flat_load, whose out-of-order
+// completion forces s_waitcnt vmcnt(0) lgkmcnt(0) before every use.
+typedef __attribute__((address_space(1))) const v4u gv4u;
+__device__ __forceinline__ v4u gload(uint64_t addr) { return *reinterpret_cast<gv4u *>(addr); }
+__device__ __forceinline__ uint4 gload4(uint64_t addr) {
+    const v4u v = gload(addr);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ uint32_t bswap16(uint32_t v) {
     return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu);
 }
@@ -99,14 +109,43 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 
-// Per-wave LDS: one 128 B slot per packet (raw chunks 0..6 of the frame on
-// the 16 B grid, then its last chunk) and the per-frame chunk sums.
+// Per-wave LDS, packet-minor ("structure of arrays") so that phase 2, where
+// lane k reads dword i of its own packet, hits 64 distinct banks: dword i of
+// packet k lives at hd[i * kHdStride + k].  Rows 0..27 hold raw chunks 0..6
+// of the frame on the 16 B grid (the headers), rows 28..31 its last chunk.
+// The odd stride also keeps phase 1's writes (7 chunks of 4 packets at once)
+// conflict-free.  sum[k] is packet k's chunk sum.
+constexpr int kHdRows = 4 * kSlotChunks;   // 32
+constexpr int kHdStride = kWave + 1;       // 65 dwords
 struct WaveLds {
-    uint4 slot[kWave][kSlotChunks];
+    uint32_t hd[kHdRows * kHdStride];
     uint32_t sum[kWave];
 };
 
-template <int MODE, bool RSS>
+// A lane's frame: address, length, descriptor validity, and its chunk range
+// [p16, p16 + 16*nch) on the absolute 16 B grid.
+struct Frame {
+    uint64_t p;
+    uint32_t L;
+    bool ok, live;
+    uint64_t p16;
+    uint32_t nch;
+};
+
+// One row-step of phase 1: kUnroll loads of 256 B per row, round i (rows take
+// frames 4i..4i+3), chunks [c0, c0 + kUnroll*16) of the row's frame.
+struct Trip {
+    int i;
+    uint32_t c0, nj;
+    uint64_t base;
+};
+
+// Packet <-> lane mapping, in passes of 64*W packets (W = waves in the grid):
+// lane k of wave w owns packet pass*64W + (k/B)*(W*B) + w*B + k%B.  B = 64:
+// each wave owns 64 consecutive packets; smaller B interleaves the waves so
+// that, round by round, the whole grid streams one compact window of frames.
+// ABL (profiling only): 1 = stop after phase 1 (store the chunk sums).
+template <int MODE, bool RSS, int ABL = 0, int B = 8>
 __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ WaveLds lds[kWavesPerBlock];
@@ -120,78 +159,172 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     const uint32_t wib = threadIdx.x >> 6;
     const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-    const uint32_t ngroups = (kp.n + kWave - 1) / kWave;
     WaveLds &wl = lds[wib];
+    const uint32_t pass_pkts = nwaves * kWave;
+    // packet index of lane l relative to the pass base
+    auto map = [&](uint32_t l) -> uint32_t {
+        return B == kWave ? wave * kWave + l : (l / B) * (nwaves * B) + wave * B + (l % B);
+    };
+    const uint32_t lane_off = map(lane);
+    const uint64_t safe = (uint64_t)(uintptr_t)(MODE == kRxPtrs ? (const void *)kp.out
+                                                               : (const void *)kp.buf);
 
-    for (uint32_t g = wave; g < ngroups; g += nwaves) {
-        const uint32_t k = g * kWave + lane;
-        const bool live = k < kp.n;
-
-        // ---------------- phase 0: descriptor -----------------------------
-        uint64_t p = (uint64_t)(uintptr_t)(MODE == kRxPtrs ? (const void *)kp.out : (const void *)kp.buf);
-        uint32_t L = 0;
-        bool desc_ok = false;
-        if (live) {
+    // ---------------- phase 0: descriptors (of the NEXT pass, prefetched) ---
+    // The raw descriptor fields are loaded one pass ahead so that their
+    // latency hides under the current pass's streaming.
+    uint64_t raw_a = 0;     // chunk mode: the 8-byte descriptor; ptrs mode: the pointer
+    uint32_t raw_b = 0;     // ptrs mode: the length
+    auto fetch = [&](uint32_t g0) {
+        const uint32_t k = g0 + lane_off;
+        if (k < kp.n) {
             if constexpr (MODE == kRxPtrs) {
-                p = (uint64_t)(uintptr_t)kp.ptrs[k];
-                L = kp.lens[k];
-                desc_ok = p != 0 && (p & 3) == 0;
-                // rows with nothing to read still issue (clamped) loads: give
-                // them an address that is always mapped
-                if (!desc_ok) p = (uint64_t)(uintptr_t)kp.out;
+                raw_a = (uint64_t)(uintptr_t)kp.ptrs[k];
+                raw_b = kp.lens[k];
             } else {
-                const mtcp_gpu_desc d = kp.desc[k];
-                const int64_t pos = (int64_t)((uint64_t)d.offset << kp.off_shift) - kp.base_sub;
-                L = d.len;
-                desc_ok = pos >= 0 && (pos & 3) == 0 && (uint64_t)pos + L <= kp.buf_len;
-                p += (uint64_t)(desc_ok ? pos : 0);
+                raw_a = *reinterpret_cast<const uint64_t *>(kp.desc + k);
             }
         }
-        // chunk range of the frame on the 16 B grid: [p16, p16 + 16*nch)
-        const uint64_t p16 = p & ~15ull;
-        const uint32_t nch = desc_ok && L ? (uint32_t)((((p + L + 15) & ~15ull) - p16) >> 4) : 0u;
+    };
+    auto decode = [&](uint32_t g0) -> Frame {
+        Frame f;
+        const uint32_t k = g0 + lane_off;
+        f.live = k < kp.n;
+        f.p = safe;
+        f.L = 0;
+        f.ok = false;
+        if (f.live) {
+            if constexpr (MODE == kRxPtrs) {
+                f.L = raw_b;
+                f.ok = raw_a != 0 && (raw_a & 3) == 0;
+                // rows with nothing to read still issue (clamped) loads: keep
+                // their address on always-mapped memory
+                if (f.ok) f.p = raw_a;
+            } else {
+                const uint32_t off = (uint32_t)raw_a;
+                f.L = (uint32_t)(raw_a >> 32) & 0xFFFFu;
+                const int64_t pos = (int64_t)((uint64_t)off << kp.off_shift) - kp.base_sub;
+                f.ok = pos >= 0 && (pos & 3) == 0 && (uint64_t)pos + f.L <= kp.buf_len;
+                if (f.ok) f.p = safe + (uint64_t)pos;
+            }
+        }
+        f.p16 = f.p & ~15ull;
+        f.nch = f.ok && f.L ? (uint32_t)((((f.p + f.L + 15) & ~15ull) - f.p16) >> 4) : 0u;
+        return f;
+    };
+
+    // ---------------- phase 1 building blocks -----------------------------
+    auto enter_round = [&](const Frame &f, Trip &t, int ii) {
+        const int j = 4 * ii + (int)row;
+        t.i = ii;
+        t.c0 = 0;
+        t.nj = shfl32(f.nch, j);
+        t.base = ((uint64_t)shfl32((uint32_t)(f.p16 >> 32), j) << 32) | shfl32((uint32_t)f.p16, j);
+    };
+    // next trip with work; false (nj = 0, base kept valid) when the pass is done
+    auto advance = [&](const Frame &f, Trip &t) -> bool {
+        if (__ballot(t.c0 + kUnroll * kRow < t.nj)) {
+            t.c0 += kUnroll * kRow;
+            return true;
+        }
+        for (int ii = t.i + 1; ii < kWave / 4; ++ii) {
+            enter_round(f, t, ii);
+            if (__ballot(t.nj != 0)) return true;
+        }
+        t.nj = 0;
+        return false;
+    };
+    auto first_trip = [&](const Frame &f, Trip &t) -> bool {
+        enter_round(f, t, 0);
+        return __ballot(t.nj != 0) || advance(f, t);
+    };
+    auto issue = [&](const Trip &t, v4u (&x)[kUnroll]) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint32_t c = t.c0 + u * kRow + rlane;
+            const uint32_t cc = c < t.nj ? c : (t.nj ? t.nj - 1 : 0u);   // clamp: no exec mask
+            x[u] = gload(t.base + 16ull * cc);
+        }
+    };
+    auto consume = [&](const Trip &t, const v4u (&x)[kUnroll], uint32_t &acc) {
+        const int j = 4 * t.i + (int)row;
+        if (t.c0 == 0 && rlane < kSlotChunks - 1) {                  // raw chunks 0..6
+            uint32_t *d = wl.hd + 4 * rlane * kHdStride + j;
+            d[0] = x[0].x; d[kHdStride] = x[0].y;
+            d[2 * kHdStride] = x[0].z; d[3 * kHdStride] = x[0].w;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint32_t c = t.c0 + u * kRow + rlane;
+            const uint32_t s = halves4(x[u], 0u);
+            acc += c < t.nj ? s : 0u;
+            if (c == t.nj - 1) {                                       // last chunk
+                uint32_t *d = wl.hd + 4 * (kSlotChunks - 1) * kHdStride + j;
+                d[0] = x[u].x; d[kHdStride] = x[u].y;
+                d[2 * kHdStride] = x[u].z; d[3 * kHdStride] = x[u].w;
+            }
+        }
+    };
+
+    fetch(0);
+    v4u X[kUnroll];
+    Trip pre;                    // next pass's first trip, already issued into X
+    bool have_pre = false;
+    for (uint32_t g0 = 0; g0 < kp.n; g0 += pass_pkts) {
+        const Frame f = decode(g0);
+        if (!__ballot(f.live)) break;
+        fetch(g0 + pass_pkts);                                     // next pass's descriptors
+        const uint32_t k = g0 + lane_off;
+        const bool live = f.live, desc_ok = f.ok;
+        const uint64_t p = f.p, p16 = f.p16;
+        const uint32_t L = f.L, nch = f.nch;
 
         // ---------------- phase 1: four frames per wave-instruction ---------
-        if (__ballot(nch != 0)) {
-            for (int i = 0; i < kWave / 4; ++i) {
-                const int j = 4 * i + (int)row;                    // this row's frame
-                const uint32_t nj = shfl32(nch, j);
-                if (!__ballot(nj != 0)) continue;
-                const uint64_t bj = ((uint64_t)shfl32((uint32_t)(p16 >> 32), j) << 32) |
-                                    shfl32((uint32_t)p16, j);
-                const uint4 *base = reinterpret_cast<const uint4 *>(bj);
-                uint32_t acc = 0;
-                for (uint32_t c0 = 0;; c0 += kUnroll * kRow) {
-                    v4u x[kUnroll];
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) {
-                        const uint32_t c = c0 + u * kRow + rlane;
-                        const uint32_t cc = c < nj ? c : (nj ? nj - 1 : 0u);   // clamp: no exec mask
-                        x[u] = *reinterpret_cast<const v4u *>(base + cc);
-                    }
-                    if (c0 == 0 && rlane < kSlotChunks - 1)              // raw chunks 0..6
-                        wl.slot[j][rlane] = make_uint4(x[0].x, x[0].y, x[0].z, x[0].w);
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) {
-                        const uint32_t c = c0 + u * kRow + rlane;
-                        const uint32_t s = halves4(x[u], 0u);
-                        acc += c < nj ? s : 0u;
-                        if (c == nj - 1) wl.slot[j][kSlotChunks - 1] = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
-                    }
-                    if (!__ballot(c0 + kUnroll * kRow < nj)) break;
+        {
+            Trip cur;
+            bool have;
+            if (have_pre) {
+                cur = pre;
+                have = true;
+            } else {
+                have = first_trip(f, cur);
+                if (have) issue(cur, X);
+            }
+            uint32_t acc = 0;
+            while (have) {
+                consume(cur, X, acc);
+                Trip nxt = cur;
+                const bool more = advance(f, nxt);
+                if (!more || nxt.i != cur.i) {                          // frame sums -> LDS
+                    acc = row_sum(acc);
+                    if (rlane == kRow - 1) wl.sum[4 * cur.i + (int)row] = acc;
+                    acc = 0;
                 }
-                acc = row_sum(acc);
-                if (rlane == kRow - 1) wl.sum[j] = acc;
+                if (!more) break;
+                issue(nxt, X);
+                cur = nxt;
+            }
+        }
+        // the next pass's first loads fly while this pass is finished
+        have_pre = false;
+        if (g0 + pass_pkts < kp.n) {
+            const Frame fn = decode(g0 + pass_pkts);
+            if (__ballot(fn.live) && first_trip(fn, pre)) {
+                issue(pre, X);
+                have_pre = true;
             }
         }
 
+        if constexpr (ABL == 1) {
+            if (live) kp.out[k].saddr = wl.sum[lane];
+            continue;
+        }
         // ---------------- phase 2: per-lane parse and finish ---------------
         const uint32_t sh = (uint32_t)(p & 15);
-        const uint32_t *raw = reinterpret_cast<const uint32_t *>(wl.slot[lane]);
-        const uint32_t *hw = raw + (sh >> 2);      // packet dword i at hw[i]
+        const uint32_t *raw = wl.hd + lane;                  // raw dword i at raw[i * kHdStride]
+        const uint32_t *hw = raw + (sh >> 2) * kHdStride;    // packet dword i at hw[i * kHdStride]
         uint32_t h[24];
 #pragma unroll
-        for (int i = 0; i < 24; ++i) h[i] = hw[i];
+        for (int i = 0; i < 24; ++i) h[i] = hw[i * kHdStride];
 
         uint32_t verdict = MTCP_GPU_V_BAD_DESC;
         uint32_t eth_type = 0, ip_len = 0, ihl = 0, ihl_doff = 0, ip_csum = 0;
@@ -244,8 +377,9 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                         if (tcp_entry) {
                             // tcp_in.c:1142-1149: tcph = iph + 4*ihl
                             const uint32_t tw = (T - 2) >> 2;
-                            const uint32_t e0 = hw[tw], e1 = hw[tw + 1], e2 = hw[tw + 2];
-                            const uint32_t e3 = hw[tw + 3], e4 = hw[tw + 4];
+                            const uint32_t *te = hw + tw * kHdStride;
+                            const uint32_t e0 = te[0], e1 = te[kHdStride], e2 = te[2 * kHdStride];
+                            const uint32_t e3 = te[3 * kHdStride], e4 = te[4 * kHdStride];
                             const uint32_t doff = (e3 >> 20) & 0xFu;
                             saddr = (h[6] >> 16) | (h[7] << 16);
                             daddr = (h[7] >> 16) | (h[8] << 16);
@@ -310,9 +444,9 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
             const int tw = pre + (int)((T - 2) >> 2);
 #pragma unroll
             for (int i = 0; i < 28; ++i) {
-                if (i < tw) s_out = halves(raw[i], s_out);
+                if (i < tw) s_out = halves(raw[i * kHdStride], s_out);
             }
-            s_out += raw[tw] & 0xFFFFu;
+            s_out += raw[tw * kHdStride] & 0xFFFFu;
             // (b) bytes [p + E, p16 + 16*nch)
             const uint64_t e_abs = p + 14 + ip_len;
             const uint64_t end = p16 + 16ull * nch;
@@ -321,8 +455,12 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
             if (te) {
                 // partial chunk: the last chunk when E and the frame end share it
                 uint4 w;
-                if (cstart + 16 == end) w = wl.slot[lane][kSlotChunks - 1];
-                else w = *reinterpret_cast<const uint4 *>(cstart);  // rare: E well before len
+                if (cstart + 16 == end) {
+                    const uint32_t *t = raw + 4 * (kSlotChunks - 1) * kHdStride;
+                    w = make_uint4(t[0], t[kHdStride], t[2 * kHdStride], t[3 * kHdStride]);
+                } else {
+                    w = gload4(cstart);                            // rare: E well before len
+                }
                 const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -333,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 cstart += 16;
             }
             for (; cstart < end; cstart += 16) {                   // rare: whole chunks past E
-                const uint4 w = *reinterpret_cast<const uint4 *>(cstart);
+                const uint4 w = gload4(cstart);
                 s_out = halves(w.w, halves(w.z, halves(w.y, halves(w.x, s_out))));
             }
             uint32_t s = wl.sum[lane] - s_out;                     // exact segment sum
@@ -356,27 +494,22 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 if (kp.fill_count) atomicAdd(kp.fill_count, 1u);
             }
         } else {
-            // stage the 64 records (2560 B) in this wave's LDS slots, then
-            // store them with full 16-byte lanes: 2.5 coalesced wave-stores
-            uint2 *st = reinterpret_cast<uint2 *>(wl.slot) + lane * 5;
+            // stage the 64 records (2560 B) in this wave's LDS, then store
+            // them as 8-byte pieces: lanes of one run of B packets write one
+            // contiguous B*40-byte span of the output
+            uint2 *st = reinterpret_cast<uint2 *>(wl.hd) + lane * 5;
             st[0] = make_uint2(saddr, daddr);
             st[1] = make_uint2(ports, seq);
             st[2] = make_uint2(ack, window | (ip_len << 16));
             st[3] = make_uint2(ip_csum | (tcp_csum << 16), rss_hash);
             st[4] = make_uint2(payload_len | (ihl_doff << 16) | (flags << 24),
                                verdict | (rss_queue << 8) | (eth_type << 16));
-            const uint32_t nrec = min((uint32_t)kWave, kp.n - g * kWave);
-            const uint4 *src = reinterpret_cast<const uint4 *>(wl.slot);
-            uint4 *dst = reinterpret_cast<uint4 *>(kp.out + (size_t)g * kWave);
-            const uint32_t n16 = nrec * 40 / 16;     // nrec * 40 is a multiple of 8
+            const uint2 *src = reinterpret_cast<const uint2 *>(wl.hd);
 #pragma unroll
-            for (uint32_t i = 0; i < 3; ++i) {
-                const uint32_t q = i * kWave + lane;
-                if (q < n16) dst[q] = src[q];
-            }
-            if ((nrec * 40) & 8) {                   // odd record count: last 8 bytes
-                if (lane == 0)
-                    reinterpret_cast<uint2 *>(dst)[n16 * 2] = reinterpret_cast<const uint2 *>(src)[n16 * 2];
+            for (uint32_t i = 0; i < 5; ++i) {
+                const uint32_t q = i * kWave + lane;      // 8-byte piece of record q/5
+                const uint32_t rec = g0 + map(q / 5);
+                if (rec < kp.n) reinterpret_cast<uint2 *>(kp.out + rec)[q % 5] = src[q];
             }
         }
     }

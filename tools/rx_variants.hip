@@ -17,6 +17,28 @@
 
 typedef void (*kfn)(mg::KParams);
 
+// Pure read-only stream over the same frame buffer (the measured ceiling on
+// THIS data): grid-stride dwordx4 + v_sad_u16, 4 loads in flight per lane.
+__global__ __launch_bounds__(256) void plain_stream(mg::KParams kp) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(kp.buf);
+    const uint64_t n16 = kp.buf_len / 16;
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 1024;
+    for (uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = (i + u * 256 < n16) ? p[i + u * 256] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            acc = __builtin_amdgcn_sad_u16(v[u].x, 0u, acc);
+            acc = __builtin_amdgcn_sad_u16(v[u].y, 0u, acc);
+            acc = __builtin_amdgcn_sad_u16(v[u].z, 0u, acc);
+            acc = __builtin_amdgcn_sad_u16(v[u].w, 0u, acc);
+        }
+    }
+    if (acc == 0x12345678u) kp.out[0].saddr = acc;
+}
+
 struct Variant { const char *name; kfn fn; uint32_t blocks_per_cu; };
 
 static uint64_t mix(uint64_t z) {
@@ -79,12 +101,18 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (rss) {
-        vs.push_back({"rss_cu4", mg::rx_kernel<mg::kRxChunk, true>, 4});
-        vs.push_back({"rss_cu2", mg::rx_kernel<mg::kRxChunk, true>, 2});
+        vs.push_back({"rss_B8_cu4", mg::rx_kernel<mg::kRxChunk, true, 0, 8>, 4});
+        vs.push_back({"rss_B8_cu2", mg::rx_kernel<mg::kRxChunk, true, 0, 8>, 2});
+        vs.push_back({"rss_B64_cu4", mg::rx_kernel<mg::kRxChunk, true, 0, 64>, 4});
     } else {
-        vs.push_back({"cu4", mg::rx_kernel<mg::kRxChunk, false>, 4});
-        vs.push_back({"cu2", mg::rx_kernel<mg::kRxChunk, false>, 2});
-        vs.push_back({"cu3", mg::rx_kernel<mg::kRxChunk, false>, 3});
+        vs.push_back({"B8_cu2", mg::rx_kernel<mg::kRxChunk, false, 0, 8>, 2});
+        vs.push_back({"B8_cu1", mg::rx_kernel<mg::kRxChunk, false, 0, 8>, 1});
+        vs.push_back({"B8_cu3", mg::rx_kernel<mg::kRxChunk, false, 0, 8>, 3});
+        vs.push_back({"B8_cu4", mg::rx_kernel<mg::kRxChunk, false, 0, 8>, 4});
+        vs.push_back({"B4_cu2", mg::rx_kernel<mg::kRxChunk, false, 0, 4>, 2});
+        vs.push_back({"B64_cu2", mg::rx_kernel<mg::kRxChunk, false, 0, 64>, 2});
+        vs.push_back({"B8_p1only_cu2", mg::rx_kernel<mg::kRxChunk, false, 1, 8>, 2});
+        vs.push_back({"plain_stream_cu2", plain_stream, 2});
     }
     if (single) vs.resize(1);
     hipEvent_t a, b;
@@ -95,7 +123,7 @@ int main(int argc, char **argv) {
     for (int r = 0; r < rounds; ++r) {
         for (size_t v = 0; v < vs.size(); ++v) {
             const uint32_t groups = (n + 63) / 64;
-            uint32_t blocks = (groups + 3) / 4;
+            uint32_t blocks = strstr(vs[v].name, "plain") ? 1u << 20 : (groups + 3) / 4;
             if (blocks > cus * vs[v].blocks_per_cu) blocks = cus * vs[v].blocks_per_cu;
             kp.out = v == 0 ? d_ref : d_out;
             CK(hipMemset(kp.out, 0, n * sizeof(mtcp_gpu_result)));
@@ -107,7 +135,7 @@ int main(int argc, char **argv) {
             float t;
             CK(hipEventElapsedTime(&t, a, b));
             ms[v].push_back(t / reps);
-            if (v > 0 && r == 0) {
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "p1only") && !strstr(vs[v].name, "plain")) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
