@@ -168,22 +168,23 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # HIP events on the launch stream bracket the timed region: average launch
+    # duration = their interval / K (back-to-back launches, no host sync between)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        e.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

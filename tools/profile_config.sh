@@ -1,0 +1,13 @@
+#!/bin/bash
+# rocprofv3 evidence for one bench config, each pass its own run:
+#   1. --kernel-trace --stats (durations)
+#   2. --pmc FETCH_SIZE          3. --pmc WRITE_SIZE
+#   4. --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum
+# usage: tools/profile_config.sh CONFIG OUTDIR
+cfg=$1; out=$2
+mkdir -p "$out"
+b="python3 bench.py --config $cfg --steps 30 --warmup 3 --cpu-baseline off --pcie off"
+rocprofv3 --kernel-trace --stats -T --output-format csv -d "$out/trace" -o run -- $b > "$out/trace.log" 2>&1 || exit $?
+rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$out/fetch" -o run -- $b > "$out/fetch.log" 2>&1 || exit $?
+rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d "$out/write" -o run -- $b > "$out/write.log" 2>&1 || exit $?
+rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum --kernel-trace -T --output-format csv -d "$out/rdreq" -o run -- $b > "$out/rdreq.log" 2>&1 || exit $?
