@@ -70,6 +70,10 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 // completion forces s_waitcnt vmcnt(0) lgkmcnt(0) before every use.
 typedef __attribute__((address_space(1))) const v4u gv4u;
 __device__ __forceinline__ v4u gload(uint64_t addr) { return *reinterpret_cast<gv4u *>(addr); }
+// Streaming (once-read) frame data: non-temporal global load.
+__device__ __forceinline__ v4u gload_nt(uint64_t addr) {
+    return __builtin_nontemporal_load(reinterpret_cast<gv4u *>(addr));
+}
 __device__ __forceinline__ uint4 gload4(uint64_t addr) {
     const v4u v = gload(addr);
     return make_uint4(v.x, v.y, v.z, v.w);
@@ -109,6 +113,17 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 
+// Lane i of each 16-lane row, broadcast to the row (DPP row_newbcast:i).
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v, int i) {
+#define MG_NB(n) case n: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + n, 0xF, 0xF, false)
+    switch (i) {
+        MG_NB(0); MG_NB(1); MG_NB(2); MG_NB(3); MG_NB(4); MG_NB(5); MG_NB(6); MG_NB(7);
+        MG_NB(8); MG_NB(9); MG_NB(10); MG_NB(11); MG_NB(12); MG_NB(13); MG_NB(14);
+        default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x15F, 0xF, 0xF, false);
+    }
+#undef MG_NB
+}
+
 // Per-wave LDS, packet-minor ("structure of arrays") so that phase 2, where
 // lane k reads dword i of its own packet, hits 64 distinct banks: dword i of
 // packet k lives at hd[i * kHdStride + k].  Rows 0..27 hold raw chunks 0..6
@@ -130,6 +145,9 @@ struct Frame {
     bool ok, live;
     uint64_t p16;
     uint32_t nch;
+    // the frame row `row` streams in round `rlane`, i.e. frame 4*rlane + row,
+    // gathered once per pass so that a round only needs a row broadcast
+    uint32_t r_nch, r_lo, r_hi;
 };
 
 // One row-step of phase 1: kUnroll loads of 256 B per row, round i (rows take
@@ -144,8 +162,10 @@ struct Trip {
 // lane k of wave w owns packet pass*64W + (k/B)*(W*B) + w*B + k%B.  B = 64:
 // each wave owns 64 consecutive packets; smaller B interleaves the waves so
 // that, round by round, the whole grid streams one compact window of frames.
-// ABL (profiling only): 1 = stop after phase 1 (store the chunk sums).
-template <int MODE, bool RSS, int ABL = 0, int B = 8>
+// ABL (profiling only): 1 = stop after phase 1 (store the chunk sums);
+// 2 = also no LDS header/tail copies; 3 = also no per-chunk range mask.
+template <int MODE, bool RSS, int ABL = 0, int B = 8, bool NT = true, int U = 6, bool PIPE = false,
+          bool PAIR = false>
 __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ WaveLds lds[kWavesPerBlock];
@@ -209,21 +229,24 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         }
         f.p16 = f.p & ~15ull;
         f.nch = f.ok && f.L ? (uint32_t)((((f.p + f.L + 15) & ~15ull) - f.p16) >> 4) : 0u;
+        const int src = 4 * (int)rlane + (int)row;
+        f.r_nch = shfl32(f.nch, src);
+        f.r_lo = shfl32((uint32_t)f.p16, src);
+        f.r_hi = shfl32((uint32_t)(f.p16 >> 32), src);
         return f;
     };
 
     // ---------------- phase 1 building blocks -----------------------------
     auto enter_round = [&](const Frame &f, Trip &t, int ii) {
-        const int j = 4 * ii + (int)row;
         t.i = ii;
         t.c0 = 0;
-        t.nj = shfl32(f.nch, j);
-        t.base = ((uint64_t)shfl32((uint32_t)(f.p16 >> 32), j) << 32) | shfl32((uint32_t)f.p16, j);
+        t.nj = row_bcast(f.r_nch, ii);
+        t.base = ((uint64_t)row_bcast(f.r_hi, ii) << 32) | row_bcast(f.r_lo, ii);
     };
     // next trip with work; false (nj = 0, base kept valid) when the pass is done
     auto advance = [&](const Frame &f, Trip &t) -> bool {
-        if (__ballot(t.c0 + kUnroll * kRow < t.nj)) {
-            t.c0 += kUnroll * kRow;
+        if (__ballot(t.c0 + U * kRow < t.nj)) {
+            t.c0 += U * kRow;
             return true;
         }
         for (int ii = t.i + 1; ii < kWave / 4; ++ii) {
@@ -237,27 +260,27 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         enter_round(f, t, 0);
         return __ballot(t.nj != 0) || advance(f, t);
     };
-    auto issue = [&](const Trip &t, v4u (&x)[kUnroll]) {
+    auto issue = [&](const Trip &t, v4u (&x)[U]) {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < U; ++u) {
             const uint32_t c = t.c0 + u * kRow + rlane;
             const uint32_t cc = c < t.nj ? c : (t.nj ? t.nj - 1 : 0u);   // clamp: no exec mask
-            x[u] = gload(t.base + 16ull * cc);
+            x[u] = NT ? gload_nt(t.base + 16ull * cc) : gload(t.base + 16ull * cc);
         }
     };
-    auto consume = [&](const Trip &t, const v4u (&x)[kUnroll], uint32_t &acc) {
+    auto consume = [&](const Trip &t, const v4u (&x)[U], uint32_t &acc) {
         const int j = 4 * t.i + (int)row;
-        if (t.c0 == 0 && rlane < kSlotChunks - 1) {                  // raw chunks 0..6
+        if (ABL < 2 && t.c0 == 0 && rlane < kSlotChunks - 1) {       // raw chunks 0..6
             uint32_t *d = wl.hd + 4 * rlane * kHdStride + j;
             d[0] = x[0].x; d[kHdStride] = x[0].y;
             d[2 * kHdStride] = x[0].z; d[3 * kHdStride] = x[0].w;
         }
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < U; ++u) {
             const uint32_t c = t.c0 + u * kRow + rlane;
             const uint32_t s = halves4(x[u], 0u);
-            acc += c < t.nj ? s : 0u;
-            if (c == t.nj - 1) {                                       // last chunk
+            acc += (ABL >= 3 || c < t.nj) ? s : 0u;
+            if (ABL < 2 && c == t.nj - 1) {                            // last chunk
                 uint32_t *d = wl.hd + 4 * (kSlotChunks - 1) * kHdStride + j;
                 d[0] = x[u].x; d[kHdStride] = x[u].y;
                 d[2 * kHdStride] = x[u].z; d[3 * kHdStride] = x[u].w;
@@ -266,7 +289,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     };
 
     fetch(0);
-    v4u X[kUnroll];
+    v4u X[U], Y[U];
     Trip pre;                    // next pass's first trip, already issued into X
     bool have_pre = false;
     for (uint32_t g0 = 0; g0 < kp.n; g0 += pass_pkts) {
@@ -277,8 +300,14 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         const bool live = f.live, desc_ok = f.ok;
         const uint64_t p = f.p, p16 = f.p16;
         const uint32_t L = f.L, nch = f.nch;
+        const bool has_next = g0 + pass_pkts < kp.n;
 
         // ---------------- phase 1: four frames per wave-instruction ---------
+        // Software pipeline: the loads of trip t+1 (or, at the end of the
+        // pass, of the next pass's first trip) are issued before trip t is
+        // consumed; X and Y alternate.  Every step issues exactly U
+        // loads (a finished pipeline loads a harmless dummy) so that the
+        // compiler's counted vmcnt waits stay exact.
         {
             Trip cur;
             bool have;
@@ -287,34 +316,105 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 have = true;
             } else {
                 have = first_trip(f, cur);
-                if (have) issue(cur, X);
+                issue(cur, X);
             }
             uint32_t acc = 0;
-            while (have) {
-                consume(cur, X, acc);
-                Trip nxt = cur;
-                const bool more = advance(f, nxt);
-                if (!more || nxt.i != cur.i) {                          // frame sums -> LDS
+            // the trip to issue after `c`: within the pass, or the next pass's first
+            auto next_of = [&](const Trip &c, Trip &n, bool &more, bool &pre_ok) {
+                n = c;
+                more = advance(f, n);
+                pre_ok = false;
+                if (!more && has_next) {
+                    const Frame fn = decode(g0 + pass_pkts);
+                    if (__ballot(fn.live) && first_trip(fn, n)) pre_ok = true;
+                }
+                if (!more && !pre_ok) n.nj = 0;                     // dummy (valid base)
+            };
+            auto round_end = [&](const Trip &c, const Trip &n, bool more) {
+                if (!more || n.i != c.i) {                          // frame sums -> LDS
                     acc = row_sum(acc);
-                    if (rlane == kRow - 1) wl.sum[4 * cur.i + (int)row] = acc;
+                    if (rlane == kRow - 1) wl.sum[4 * c.i + (int)row] = acc;
                     acc = 0;
                 }
-                if (!more) break;
-                issue(nxt, X);
-                cur = nxt;
+            };
+            have_pre = false;
+            if constexpr (!PIPE) {
+                // one trip (PAIR: two trips) at a time; only the next pass's
+                // first trip is issued early (before this pass's phase 2)
+                while (have) {
+                    Trip n = cur;
+                    bool more = advance(f, n);
+                    if constexpr (PAIR) {
+                        if (!more) n.nj = 0;                        // dummy: keeps vmcnt exact
+                        issue(n, Y);                                // both trips in flight
+                    }
+                    consume(cur, X, acc);
+                    round_end(cur, n, more);
+                    if (!more) break;
+                    if constexpr (PAIR) {
+                        cur = n;
+                        consume(cur, Y, acc);
+                        n = cur;
+                        more = advance(f, n);
+                        round_end(cur, n, more);
+                        if (!more) break;
+                    }
+                    issue(n, X);
+                    cur = n;
+                }
+                if (has_next) {
+                    Trip n;
+                    const Frame fn = decode(g0 + pass_pkts);
+                    if (__ballot(fn.live) && first_trip(fn, n)) {
+                        issue(n, X);
+                        pre = n;
+                        have_pre = true;
+                    }
+                }
+                have = false;
             }
-        }
-        // the next pass's first loads fly while this pass is finished
-        have_pre = false;
-        if (g0 + pass_pkts < kp.n) {
-            const Frame fn = decode(g0 + pass_pkts);
-            if (__ballot(fn.live) && first_trip(fn, pre)) {
-                issue(pre, X);
-                have_pre = true;
+            while (have) {
+                Trip n;
+                bool more, pre_ok;
+                next_of(cur, n, more, pre_ok);
+                issue(n, Y);
+                consume(cur, X, acc);
+                round_end(cur, n, more);
+                if (!more) {
+                    if (pre_ok) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) X[u] = Y[u];
+                        pre = n;
+                        have_pre = true;
+                    }
+                    break;
+                }
+                cur = n;
+                next_of(cur, n, more, pre_ok);
+                issue(n, X);
+                consume(cur, Y, acc);
+                round_end(cur, n, more);
+                if (!more) {
+                    if (pre_ok) {
+                        pre = n;
+                        have_pre = true;
+                    }
+                    break;
+                }
+                cur = n;
+            }
+            if (PIPE && !have && has_next) {  // nothing in this pass: start the next one
+                Trip n;
+                const Frame fn = decode(g0 + pass_pkts);
+                if (__ballot(fn.live) && first_trip(fn, n)) {
+                    issue(n, X);
+                    pre = n;
+                    have_pre = true;
+                }
             }
         }
 
-        if constexpr (ABL == 1) {
+        if constexpr (ABL >= 1) {
             if (live) kp.out[k].saddr = wl.sum[lane];
             continue;
         }

@@ -5,7 +5,8 @@
 #include <stdio.h>
 #include <stdint.h>
 
-template <int R, int NLOAD>
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+template <int R, int NLOAD, bool NT>
 __global__ __launch_bounds__(256) void walk(const uint4 *__restrict__ p, uint32_t nframes,
                                             uint32_t *out) {
     constexpr int LPR = 64 / R;                      // lanes per row
@@ -21,7 +22,12 @@ __global__ __launch_bounds__(256) void walk(const uint4 *__restrict__ p, uint32_
             for (int u = 0; u < NLOAD; ++u) {
                 uint32_t c = u * LPR + rl;
                 c = c < 94 ? c : 93;
-                v[u] = fr[c];
+                if (NT) {
+                    const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(fr + c));
+                    v[u] = make_uint4(w.x, w.y, w.z, w.w);
+                } else {
+                    v[u] = fr[c];
+                }
             }
 #pragma unroll
             for (int u = 0; u < NLOAD; ++u) {
@@ -35,14 +41,14 @@ __global__ __launch_bounds__(256) void walk(const uint4 *__restrict__ p, uint32_
     if (acc == 0x12345678u) out[0] = acc;
 }
 
-template <int R, int NLOAD>
+template <int R, int NLOAD, bool NT>
 void run(const char *name, const uint4 *p, uint32_t nframes, uint32_t *out, int blocks) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    for (int i = 0; i < 2; ++i) walk<R, NLOAD><<<blocks, 256>>>(p, nframes, out);
+    for (int i = 0; i < 2; ++i) walk<R, NLOAD, NT><<<blocks, 256>>>(p, nframes, out);
     (void)hipEventRecord(a);
-    for (int i = 0; i < 10; ++i) walk<R, NLOAD><<<blocks, 256>>>(p, nframes, out);
+    for (int i = 0; i < 10; ++i) walk<R, NLOAD, NT><<<blocks, 256>>>(p, nframes, out);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     float ms;
@@ -57,11 +63,13 @@ int main() {
     uint32_t *out;
     if (hipMalloc(&p, (size_t)nframes * 1536) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
     (void)hipMemset(p, 0x5a, (size_t)nframes * 1536);
-    for (int blocks : {512, 1024}) {
-        run<1, 2>("1 frame x 1KiB/instr", p, nframes, out, blocks);
-        run<2, 3>("2 frames x 512B", p, nframes, out, blocks);
-        run<4, 6>("4 frames x 256B", p, nframes, out, blocks);
-        run<8, 12>("8 frames x 128B", p, nframes, out, blocks);
+    for (int blocks : {512, 768}) {
+        run<1, 2, false>("1 frame x 1KiB/instr", p, nframes, out, blocks);
+        run<4, 6, false>("4 frames x 256B", p, nframes, out, blocks);
+        run<1, 2, true>("NT 1 frame x 1KiB/instr", p, nframes, out, blocks);
+        run<2, 3, true>("NT 2 frames x 512B", p, nframes, out, blocks);
+        run<4, 6, true>("NT 4 frames x 256B", p, nframes, out, blocks);
+        run<8, 12, true>("NT 8 frames x 128B", p, nframes, out, blocks);
     }
     return 0;
 }

@@ -17,6 +17,21 @@
 
 typedef void (*kfn)(mg::KParams);
 
+__global__ __launch_bounds__(256) void plain_stream_nt(mg::KParams kp) {
+    const uint64_t base = (uint64_t)(uintptr_t)kp.buf;
+    const uint64_t n16 = kp.buf_len / 16;
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 1024;
+    for (uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
+        mg::v4u v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = mg::gload_nt(base + 16 * ((i + u * 256 < n16) ? i + u * 256 : i));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = mg::halves4(v[u], acc);
+    }
+    if (acc == 0x12345678u) kp.out[0].saddr = acc;
+}
+
 // Pure read-only stream over the same frame buffer (the measured ceiling on
 // THIS data): grid-stride dwordx4 + v_sad_u16, 4 loads in flight per lane.
 __global__ __launch_bounds__(256) void plain_stream(mg::KParams kp) {
@@ -100,19 +115,16 @@ int main(int argc, char **argv) {
     kp.rss_endian = 1;
 
     std::vector<Variant> vs;
+    using namespace mg;
     if (rss) {
-        vs.push_back({"rss_B8_cu4", mg::rx_kernel<mg::kRxChunk, true, 0, 8>, 4});
-        vs.push_back({"rss_B8_cu2", mg::rx_kernel<mg::kRxChunk, true, 0, 8>, 2});
-        vs.push_back({"rss_B64_cu4", mg::rx_kernel<mg::kRxChunk, true, 0, 64>, 4});
+        vs.push_back({"rss_U6_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false>, 4});
     } else {
-        vs.push_back({"B8_cu2", mg::rx_kernel<mg::kRxChunk, false, 0, 8>, 2});
-        vs.push_back({"B8_cu1", mg::rx_kernel<mg::kRxChunk, false, 0, 8>, 1});
-        vs.push_back({"B8_cu3", mg::rx_kernel<mg::kRxChunk, false, 0, 8>, 3});
-        vs.push_back({"B8_cu4", mg::rx_kernel<mg::kRxChunk, false, 0, 8>, 4});
-        vs.push_back({"B4_cu2", mg::rx_kernel<mg::kRxChunk, false, 0, 4>, 2});
-        vs.push_back({"B64_cu2", mg::rx_kernel<mg::kRxChunk, false, 0, 64>, 2});
-        vs.push_back({"B8_p1only_cu2", mg::rx_kernel<mg::kRxChunk, false, 1, 8>, 2});
-        vs.push_back({"plain_stream_cu2", plain_stream, 2});
+        vs.push_back({"U6_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false>, 2});
+        vs.push_back({"abl1_p1only", rx_kernel<kRxChunk, false, 1, 8, true, 6, false>, 2});
+        vs.push_back({"abl2_nolds", rx_kernel<kRxChunk, false, 2, 8, true, 6, false>, 2});
+        vs.push_back({"abl3_nomask", rx_kernel<kRxChunk, false, 3, 8, true, 6, false>, 2});
+        vs.push_back({"abl3_nomask_cu3", rx_kernel<kRxChunk, false, 3, 8, true, 6, false>, 3});
+        vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     }
     if (single) vs.resize(1);
     hipEvent_t a, b;
@@ -135,7 +147,7 @@ int main(int argc, char **argv) {
             float t;
             CK(hipEventElapsedTime(&t, a, b));
             ms[v].push_back(t / reps);
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "p1only") && !strstr(vs[v].name, "plain")) {
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "plain")) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
