@@ -6,8 +6,8 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
 LIB      := mtcp_amd/lib/libmtcp_gpu.so
-SRCS     := mtcp_amd/csrc/mtcp_gpu.hip mtcp_amd/csrc/pktgen.hip
-DEPS     := $(SRCS) mtcp_amd/csrc/rx_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h
+SRCS     := mtcp_amd/csrc/mtcp_gpu.hip mtcp_amd/csrc/pktgen.hip mtcp_amd/csrc/rxq.hip
+DEPS     := $(SRCS) mtcp_amd/csrc/rx_kernels.hpp mtcp_amd/csrc/flow_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h include/mtcp_gpu_rxq.h
 
 .PHONY: all lib oracle ref golden examples clean tools
 
@@ -39,3 +39,9 @@ tools/hbm_ceiling: tools/hbm_ceiling.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -w -o $@ $<
 
 tools: tools/rx_variants tools/hbm_ceiling
+
+# gpu_module.c driven by the RunMainLoop rx harness; the
+# mTCP types come from the test doubles in tests/c/mtcp_double.
+tests/c/rxloop: tests/c/rxloop.c mtcp_amd/io_module/gpu_module.c include/mtcp_gpu_rxq.h $(LIB)
+	gcc -std=gnu99 -O2 -Wall -Itests/c/mtcp_double -Iinclude -o $@ tests/c/rxloop.c \
+	    mtcp_amd/io_module/gpu_module.c -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib'

@@ -28,6 +28,12 @@
  *       the DISABLE_HWCSUM checksum fills of the tx path:
  *       iph->check = ip_fast_csum(iph, iph->ihl)   (mtcp/src/ip_out.c:94,164)
  *       tcph->check = TCPCalcChecksum(...)          (mtcp/src/tcp_out.c:211,329)
+ *   mtcp_gpu_flow_hash / _flow_hash_dev
+ *       HashFlow (mtcp/src/tcp_stream.c:56-90) of the flow-table lookup key
+ *       (mtcp/src/tcp_in.c:1180-1186), the step after the checksums.
+ *   mtcp_gpu_addr_pool_search / _rss_queue_map_dev
+ *       the RSS-friendly address search of CreateAddressPoolPerCore
+ *       (mtcp/src/addr_pool.c:155-178) over GetRSSCPUCore (mtcp/src/rss.c:90-103).
  *   mtcp_gpu_dev_ioctl
  *       io_module_func.dev_ioctl (mtcp/src/include/io_module.h:67) for the
  *       checksum commands PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM / PKT_TX_IP_CSUM /
@@ -222,6 +228,60 @@ int mtcp_gpu_tx_fill_dev(mtcp_gpu_ctx *ctx, void *d_buf, uint64_t buf_len,
 int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len,
                      const mtcp_gpu_desc *desc, uint32_t n, uint32_t off_shift,
                      uint32_t *n_filled);
+
+/* ---- flow-table hash (HashFlow) --------------------------------------- */
+#define MTCP_GPU_NUM_BINS_FLOWS  131072u      /* mtcp/src/include/fhash.h:7 */
+#define MTCP_GPU_FLOW_NONE       0xFFFFFFFFu  /* packet never reaches the flow table */
+
+/*
+ * Flow-table bin of every rx result: HashFlow (mtcp/src/tcp_stream.c:56-90,
+ * Jenkins one-at-a-time over signed chars, masked to NUM_BINS_FLOWS - 1) of
+ * the stream key ProcessTCPPacket hands to StreamHTSearch
+ * (mtcp/src/tcp_in.c:1180-1186): saddr = iph->daddr, daddr = iph->saddr,
+ * sport = tcph->dest, dport = tcph->source.  Results whose verdict is not
+ * MTCP_GPU_V_TCP_OK get MTCP_GPU_FLOW_NONE.  This is the step right after the
+ * checksum; CreateHashtable(HashFlow, ...) at mtcp/src/core.c:899.
+ */
+int mtcp_gpu_flow_hash_dev(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *d_res, uint32_t n,
+                           uint32_t *d_bins, void *stream);
+int mtcp_gpu_flow_hash(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *res, uint32_t n,
+                       uint32_t *bins);
+
+/* ---- RSS-friendly source address pool --------------------------------- */
+#define MTCP_GPU_MIN_PORT 1025u               /* mtcp/src/include/addr_pool.h:7 */
+#define MTCP_GPU_MAX_PORT 65536u              /* mtcp/src/include/addr_pool.h:8 */
+
+/* One pool entry: sockaddr_in's address and port, network order. */
+typedef struct mtcp_gpu_addr_entry {
+    uint32_t saddr;
+    uint16_t sport;
+    uint16_t rsvd;
+} mtcp_gpu_addr_entry;
+
+/*
+ * RSS queue of every candidate (source address, source port) of an active
+ * opener: d_queue[i * (MAX_PORT - MIN_PORT) + (port - MIN_PORT)] =
+ * GetRSSCPUCore(daddr_h, saddr_base_h + i, dport_h, port, num_queues,
+ * endian_check) (mtcp/src/rss.c:90-103) with the context's Toeplitz key, for
+ * i < num_addr and MIN_PORT <= port < MAX_PORT.  Host-order arguments.
+ */
+int mtcp_gpu_rss_queue_map_dev(mtcp_gpu_ctx *ctx, uint32_t saddr_base_h, uint32_t num_addr,
+                               uint32_t daddr_h, uint16_t dport_h, int num_queues,
+                               int endian_check, uint8_t *d_queue, void *stream);
+
+/*
+ * The search of CreateAddressPoolPerCore (mtcp/src/addr_pool.c:103-180): the
+ * candidates whose RSS queue is `core`, in (address, port) order, at most
+ * num_addr * (MAX_PORT - MIN_PORT) / num_queues of them (addr_pool.c:129).
+ * saddr_base, daddr and dport are network order, as the reference's
+ * arguments.  Writes min(count, max_out) entries to host memory `out` and the
+ * count the reference keeps to *n_found.  Synchronous.
+ */
+int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues,
+                              uint32_t saddr_base, int num_addr, uint32_t daddr,
+                              uint16_t dport, int endian_check,
+                              mtcp_gpu_addr_entry *out, uint32_t max_out,
+                              uint32_t *n_found);
 
 /* Pin / unpin host memory for DMA and zero-copy device access
  * (hipHostRegister; the pattern SURVEY §7 names for DPDK mempools). */

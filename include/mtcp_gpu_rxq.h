@@ -1,0 +1,79 @@
+/*
+ * mtcp_gpu_rxq.h — burst aggregation for a GPU-offload io_module backend
+ * (SURVEY §8 f2).  Plain C ABI, part of libmtcp_gpu.so.
+ *
+ * mTCP's rx loop (RunMainLoop, mtcp/src/core.c:763-777) asks the I/O module
+ * for a burst (recv_pkts, io_module.h:63), then for each packet's pointer
+ * (get_rptr, io_module.h:62), and counts a NULL pointer as rx_errors
+ * (core.c:771-775).  Real bursts are <= 64 packets (PS_CHUNK_SIZE
+ * psio_module.c:15, MAX_PKT_BURST dpdk_module.c:71), too small for one GPU
+ * launch each, and the wrapped backend recycles its buffers on the next
+ * receive (psio_module.c:244-246, dpdk_module.c:395-398).  An rxq therefore
+ * copies the frames of several bursts into pinned staging laid out like a
+ * PSIO chunk (64 B aligned, io_engine/lib/pslib.c:146), runs the rx kernel
+ * over the aggregate once (mtcp_gpu_rx_chunk), and then answers get_rptr
+ * from the staging copy:
+ *
+ *   - MTCP_GPU_V_IP_CSUM_BAD, MTCP_GPU_V_TCP_CSUM_BAD -> NULL, exactly the
+ *     packets the reference's software checksums drop with ERROR
+ *     (ip_in.c:35-36, tcp_in.c:1167-1173), the dpdk_get_rptr pattern for
+ *     NIC-verified checksums (dpdk_module.c:473-479);
+ *   - every other verdict -> the frame, and mTCP's own code takes its usual
+ *     branch (the checks before and around the checksums stay in mTCP), with
+ *     dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answering 0
+ *     (ip_in.c:29-31, tcp_in.c:1160-1164) so the checksum is not recomputed.
+ *
+ * One rxq per mTCP thread, like its mtcp_gpu_ctx; not re-entrant.
+ */
+#ifndef MTCP_GPU_RXQ_H
+#define MTCP_GPU_RXQ_H
+
+#include <stdint.h>
+
+#include "mtcp_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTCP_GPU_ENOSPC (-28)   /* the staging area is full: flush first */
+
+typedef struct mtcp_gpu_rxq mtcp_gpu_rxq;
+
+/* Staging for up to max_pkts frames / max_bytes (64 B aligned) bytes. */
+int  mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts,
+                         uint64_t max_bytes);
+void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q);
+
+/* Copy one received frame (get_rptr's pointer and *len) into staging. */
+int  mtcp_gpu_rxq_push(mtcp_gpu_rxq *q, const uint8_t *frame, uint16_t len);
+
+/* Copy a whole PSIO chunk: frame i at buf + (info[i].offset << off_shift),
+ * length info[i].len (struct ps_chunk, io_engine/include/ps.h:187-200). */
+int  mtcp_gpu_rxq_push_chunk(mtcp_gpu_rxq *q, const uint8_t *buf, const mtcp_gpu_desc *info,
+                             uint32_t cnt, uint32_t off_shift);
+
+/* Frames staged and not yet flushed. */
+uint32_t mtcp_gpu_rxq_pending(const mtcp_gpu_rxq *q);
+
+/* Run the rx kernel over everything staged since the last reset; *n = the
+ * number of frames now served by mtcp_gpu_rxq_get (synchronous). */
+int  mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n);
+
+/* get_rptr for flushed frame i: the staged frame and its length, or NULL for
+ * the checksum failures listed above.  *res (may be NULL) receives the
+ * frame's full result record. */
+uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
+                          const mtcp_gpu_result **res);
+
+/* The staged copy of frame i (flushed or not), without a verdict: what a
+ * backend serves when the GPU is unavailable and dev_ioctl answers -1. */
+uint8_t *mtcp_gpu_rxq_frame(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len);
+
+/* Drop all staged and flushed frames (the next burst reuses the staging). */
+void mtcp_gpu_rxq_reset(mtcp_gpu_rxq *q);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

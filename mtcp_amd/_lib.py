@@ -17,7 +17,10 @@ EXPORTS = (
     "mtcp_gpu_close", "mtcp_gpu_dev_ioctl", "mtcp_gpu_stream", "mtcp_gpu_rx_chunk_dev",
     "mtcp_gpu_rx_ptrs_dev", "mtcp_gpu_rx_chunk", "mtcp_gpu_rx_ptrs", "mtcp_gpu_tx_fill_dev",
     "mtcp_gpu_tx_fill", "mtcp_gpu_host_register", "mtcp_gpu_host_unregister", "mtcp_gpu_sync",
-    "mtcp_gpu_pktgen_dev",
+    "mtcp_gpu_flow_hash_dev", "mtcp_gpu_flow_hash", "mtcp_gpu_rss_queue_map_dev",
+    "mtcp_gpu_addr_pool_search", "mtcp_gpu_pktgen_dev",
+    "mtcp_gpu_rxq_create", "mtcp_gpu_rxq_destroy", "mtcp_gpu_rxq_push", "mtcp_gpu_rxq_push_chunk",
+    "mtcp_gpu_rxq_pending", "mtcp_gpu_rxq_flush", "mtcp_gpu_rxq_get", "mtcp_gpu_rxq_frame", "mtcp_gpu_rxq_reset",
 )
 
 _lib = None
@@ -58,7 +61,22 @@ def lib() -> ctypes.CDLL:
         "mtcp_gpu_tx_fill": ([vp, vp, u64, vp, u32, u32, ctypes.POINTER(u32)], i32),
         "mtcp_gpu_host_register": ([vp, u64], i32),
         "mtcp_gpu_host_unregister": ([vp], i32),
+        "mtcp_gpu_flow_hash_dev": ([vp, vp, u32, vp, vp], i32),
+        "mtcp_gpu_flow_hash": ([vp, vp, u32, vp], i32),
+        "mtcp_gpu_rss_queue_map_dev": ([vp, u32, u32, u32, ctypes.c_uint16, i32, i32, vp, vp],
+                                       i32),
+        "mtcp_gpu_addr_pool_search": ([vp, i32, i32, u32, i32, u32, ctypes.c_uint16, i32, vp, u32,
+                                       ctypes.POINTER(u32)], i32),
         "mtcp_gpu_pktgen_dev": ([vp, u64, vp, u32, u32, u64, u64, vp], i32),
+        "mtcp_gpu_rxq_create": ([ctypes.POINTER(vp), vp, u32, u64], i32),
+        "mtcp_gpu_rxq_destroy": ([vp], None),
+        "mtcp_gpu_rxq_push": ([vp, vp, ctypes.c_uint16], i32),
+        "mtcp_gpu_rxq_push_chunk": ([vp, vp, vp, u32, u32], i32),
+        "mtcp_gpu_rxq_pending": ([vp], u32),
+        "mtcp_gpu_rxq_flush": ([vp, ctypes.POINTER(u32)], i32),
+        "mtcp_gpu_rxq_get": ([vp, u32, ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(vp)], vp),
+        "mtcp_gpu_rxq_frame": ([vp, u32, ctypes.POINTER(ctypes.c_uint16)], vp),
+        "mtcp_gpu_rxq_reset": ([vp], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

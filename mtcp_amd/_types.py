@@ -17,3 +17,11 @@ assert DESC_DTYPE.itemsize == 8 and RESULT_DTYPE.itemsize == 40
 VERDICTS = ("TCP_OK", "ETH_OTHER", "ARP", "IP_SHORT", "IP_CSUM_BAD", "IP_VERSION", "ICMP",
             "IP_PROTO_OTHER", "TCP_LEN_BAD", "TCP_CSUM_BAD", "TRUNCATED", "BAD_DESC")
 RX_ERROR_VERDICTS = (3, 4, 8, 9)   # ProcessPacket ret < 0 (eth_in.c:49-53)
+
+# struct mtcp_gpu_addr_entry: sockaddr_in address and port, network order
+ADDR_ENTRY_DTYPE = np.dtype([("saddr", "<u4"), ("sport", "<u2"), ("rsvd", "<u2")])
+assert ADDR_ENTRY_DTYPE.itemsize == 8
+
+NUM_BINS_FLOWS = 131072      # mtcp/src/include/fhash.h:7
+FLOW_NONE = 0xFFFFFFFF
+MIN_PORT, MAX_PORT = 1025, 65536   # mtcp/src/include/addr_pool.h:7-8

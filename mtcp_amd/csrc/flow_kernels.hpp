@@ -1,0 +1,207 @@
+// flow_kernels.hpp — gfx950 kernels for the two rows SURVEY §8(f) puts next
+// to the rx path:
+//
+//   f3  HashFlow (mtcp/src/tcp_stream.c:56-90) of the stream key every TCP_OK
+//       packet is looked up with (mtcp/src/tcp_in.c:1180-1186);
+//   f4  the RSS-friendly source-address search of CreateAddressPoolPerCore
+//       (mtcp/src/addr_pool.c:103-180): GetRSSCPUCore (mtcp/src/rss.c:90-103)
+//       over every (address, port) candidate, then an order-preserving
+//       compaction of the candidates that land on one core's queue.
+//
+// Both are small integer kernels: flow_hash reads 16 B of each 40 B result
+// record and writes 4 B (HBM-bound, like rx); the pool search is a Toeplitz
+// hash per candidate through the same LDS nibble tables as rx, then a
+// count / scan / emit compaction that keeps the reference's order.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mtcp_gpu.h"
+#include "rx_kernels.hpp"
+
+namespace mg {
+
+constexpr uint32_t kPorts = MTCP_GPU_MAX_PORT - MTCP_GPU_MIN_PORT;   // 64511
+constexpr int kPoolPerThread = 16;                                   // candidates per lane
+constexpr int kPoolTile = kBlock * kPoolPerThread;                   // per workgroup
+
+// Jenkins one-at-a-time over the 12 key bytes, each read as a signed char
+// (tcp_stream.c:77-87 `char *key`; x86 char is signed).  The bytes of w are
+// key bytes 4q..4q+3 in memory order.
+__device__ __forceinline__ uint32_t hash_flow(const uint32_t (&w)[3]) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        h += (uint32_t)(int32_t)(int8_t)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        h += h << 10;
+        h ^= h >> 6;
+    }
+    h += h << 3;
+    h ^= h >> 11;
+    h += h << 15;
+    return h & (MTCP_GPU_NUM_BINS_FLOWS - 1);
+}
+
+// One lane per result record: saddr @0, daddr @4, sport|dport @8, verdict @36.
+__global__ __launch_bounds__(kBlock) void flow_hash_kernel(const mtcp_gpu_result *__restrict__ res,
+                                                           uint32_t n, uint32_t *__restrict__ bins) {
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const uint32_t *r = reinterpret_cast<const uint32_t *>(res + i);
+        const uint32_t saddr = r[0], daddr = r[1], ports = r[2];
+        const uint32_t verdict = r[9] & 0xFFu;
+        // tcp_in.c:1180-1183: {saddr = iph->daddr, daddr = iph->saddr,
+        //                      sport = tcph->dest, dport = tcph->source}
+        const uint32_t w[3] = {daddr, saddr, (ports >> 16) | (ports << 16)};
+        bins[i] = verdict == MTCP_GPU_V_TCP_OK ? hash_flow(w) : MTCP_GPU_FLOW_NONE;
+    }
+}
+
+// GetRSSHash (mtcp/src/rss.c:44-82) of host-order (sip, dip, sp, dp) through
+// the 24 nibble tables: nibble t of the 96-bit input sip|dip|sp|dp, most
+// significant first, selects tables[t][nibble].
+__device__ __forceinline__ uint32_t toeplitz96(const uint32_t *tab, uint32_t sip, uint32_t dip,
+                                               uint32_t ports) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        h ^= tab[(t << 4) | ((sip >> (28 - 4 * t)) & 15u)];
+        h ^= tab[((8 + t) << 4) | ((dip >> (28 - 4 * t)) & 15u)];
+        h ^= tab[((16 + t) << 4) | ((ports >> (28 - 4 * t)) & 15u)];
+    }
+    return h;
+}
+
+// mtcp/src/rss.c:90-103: masked = hash & 0x7F, endian fix off[m & 3] =
+// {3, 1, -1, -3} (i.e. m ^ 3), queue = masked % num_queues.
+__device__ __forceinline__ uint32_t rss_queue(uint32_t h, uint32_t nq, uint32_t endian) {
+    uint32_t m = h & 0x7Fu;
+    if (endian) m ^= 3u;
+    return m % nq;
+}
+
+struct PoolParams {
+    const uint32_t *rss_tables;
+    uint32_t saddr_base_h;   // candidate i's address: saddr_base_h + i
+    uint32_t daddr_h;
+    uint32_t dport_h;
+    uint32_t nq;
+    uint32_t endian;
+    uint64_t total;          // num_addr * kPorts candidates
+};
+
+// queue[g] for candidate g = i * kPorts + (port - MIN_PORT).  The reference
+// calls GetRSSCPUCore(daddr_h, saddr_h, dport_h, sport_h, ...)
+// (addr_pool.c:164): the peer's side comes first, as the incoming packets
+// of the connection will carry it.  Four candidates per lane, one dword store.
+__global__ __launch_bounds__(kBlock) void rss_queue_map_kernel(PoolParams pp,
+                                                               uint8_t *__restrict__ queue) {
+    __shared__ uint32_t tab[kRssTableWords];
+    for (int i = threadIdx.x; i < kRssTableWords; i += kBlock) tab[i] = pp.rss_tables[i];
+    __syncthreads();
+    const uint64_t quads = (pp.total + 3) / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x; q < quads; q += stride) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint64_t g = 4 * q + b;
+            if (g < pp.total) {
+                const uint32_t i = (uint32_t)(g / kPorts);
+                const uint32_t port = MTCP_GPU_MIN_PORT + (uint32_t)(g - (uint64_t)i * kPorts);
+                const uint32_t h = toeplitz96(tab, pp.daddr_h, pp.saddr_base_h + i,
+                                              (pp.dport_h << 16) | port);
+                word |= rss_queue(h, pp.nq, pp.endian) << (8 * b);
+            }
+        }
+        if (4 * q + 3 < pp.total) {
+            reinterpret_cast<uint32_t *>(queue)[q] = word;
+        } else {
+            for (int b = 0; 4 * q + b < pp.total; ++b) queue[4 * q + b] = (uint8_t)(word >> (8 * b));
+        }
+    }
+}
+
+// Matches of lane `t` of tile `blk`: candidates [blk*kPoolTile + 16t, +16).
+__device__ __forceinline__ uint32_t pool_lane_mask(const uint8_t *queue, uint64_t total,
+                                                   uint32_t core, uint64_t first) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < kPoolPerThread; ++k)
+        if (first + k < total && queue[first + k] == core) m |= 1u << k;
+    return m;
+}
+
+// Exclusive prefix of v over the workgroup (4 waves); returns the total.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t &excl) {
+    __shared__ uint32_t wsum[kWavesPerBlock];
+    const uint32_t lane = threadIdx.x & (kWave - 1), wib = threadIdx.x / kWave;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, kWave);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == kWave - 1) wsum[wib] = x;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (int w = 0; w < kWavesPerBlock; ++w) {
+        if (w < (int)wib) before += wsum[w];
+        total += wsum[w];
+    }
+    excl = before + x - v;
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(kBlock) void pool_count_kernel(const uint8_t *__restrict__ queue,
+                                                            uint64_t total, uint32_t core,
+                                                            uint32_t *__restrict__ counts) {
+    const uint64_t first = (uint64_t)blockIdx.x * kPoolTile + (uint64_t)threadIdx.x * kPoolPerThread;
+    const uint32_t c = __popc(pool_lane_mask(queue, total, core, first));
+    uint32_t excl;
+    const uint32_t tot = block_exclusive_scan(c, excl);
+    if (threadIdx.x == 0) counts[blockIdx.x] = tot;
+}
+
+// In place exclusive scan of counts[0..nb) by one workgroup; counts[nb] = sum.
+__global__ __launch_bounds__(kBlock) void pool_scan_kernel(uint32_t *counts, uint32_t nb) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < nb ? counts[i] : 0u;
+        uint32_t excl;
+        const uint32_t tot = block_exclusive_scan(v, excl);
+        if (i < nb) counts[i] = carry + excl;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) counts[nb] = carry;
+}
+
+// Writes entry r (global rank among matches) for r < limit.
+__global__ __launch_bounds__(kBlock) void pool_emit_kernel(const uint8_t *__restrict__ queue,
+                                                           uint64_t total, uint32_t core,
+                                                           const uint32_t *__restrict__ offsets,
+                                                           uint32_t saddr_base_h, uint32_t limit,
+                                                           mtcp_gpu_addr_entry *__restrict__ out) {
+    const uint64_t first = (uint64_t)blockIdx.x * kPoolTile + (uint64_t)threadIdx.x * kPoolPerThread;
+    uint32_t m = pool_lane_mask(queue, total, core, first);
+    uint32_t excl;
+    (void)block_exclusive_scan(__popc(m), excl);
+    uint32_t r = offsets[blockIdx.x] + excl;
+    while (m && r < limit) {
+        const int k = __ffs(m) - 1;
+        m &= m - 1;
+        const uint64_t g = first + k;
+        const uint32_t i = (uint32_t)(g / kPorts);
+        const uint32_t port = MTCP_GPU_MIN_PORT + (uint32_t)(g - (uint64_t)i * kPorts);
+        mtcp_gpu_addr_entry e;
+        e.saddr = __builtin_bswap32(saddr_base_h + i);                  // htonl (addr_pool.c:158)
+        e.sport = (uint16_t)(((port & 0xFFu) << 8) | (port >> 8));      // htons (addr_pool.c:168)
+        e.rsvd = 0;
+        out[r++] = e;
+    }
+}
+
+}  // namespace mg

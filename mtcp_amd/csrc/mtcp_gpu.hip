@@ -7,6 +7,7 @@
 // (mtcp/src/ip_in.c:29-31, tcp_in.c:1160-1164).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -14,6 +15,7 @@
 #include <new>
 
 #include "../../include/mtcp_gpu.h"
+#include "flow_kernels.hpp"
 #include "rx_kernels.hpp"
 
 namespace {
@@ -51,7 +53,14 @@ struct mtcp_gpu_ctx {
 
 namespace {
 
-#define HIP_OK(x) ((x) == hipSuccess)
+// MTCP_GPU_DEBUG=1 in the environment: report every failing HIP call.
+bool hip_ok(hipError_t e, const char *what) {
+    if (e == hipSuccess) return true;
+    static const bool debug = getenv("MTCP_GPU_DEBUG") != nullptr;
+    if (debug) fprintf(stderr, "mtcp_gpu: %s -> %s\n", what, hipGetErrorString(e));
+    return false;
+}
+#define HIP_OK(x) hip_ok((x), #x)
 
 // util/rss.c:13-105 (BuildKeyCache), then the 24 nibble tables the kernel
 // XORs: table[t][v] = XOR of cache[4t + m] over the bits of nibble v, MSB
@@ -442,6 +451,117 @@ int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mt
         rc = MTCP_GPU_EIO;
     if (!HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK) rc = MTCP_GPU_EIO;
     if (rc == MTCP_GPU_OK && n_filled) *n_filled = cnt;
+    return rc;
+}
+
+// ---- flow-table hash --------------------------------------
+int mtcp_gpu_flow_hash_dev(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *d_res, uint32_t n,
+                           uint32_t *d_bins, void *stream) {
+    if (!ctx || (n && (!d_res || !d_bins)) || ((uintptr_t)d_res & 7) || ((uintptr_t)d_bins & 3))
+        return MTCP_GPU_EINVAL;
+    if (n == 0) return MTCP_GPU_OK;
+    (void)hipSetDevice(ctx->device);
+    const uint32_t blocks = std::min<uint32_t>((n + mg::kBlock - 1) / mg::kBlock,
+                                               (uint32_t)ctx->num_cu * 8);
+    hipLaunchKernelGGL(mg::flow_hash_kernel, dim3(blocks), dim3(mg::kBlock), 0, pick(ctx, stream),
+                       d_res, n, d_bins);
+    return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
+}
+
+int mtcp_gpu_flow_hash(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *res, uint32_t n,
+                       uint32_t *bins) {
+    if (!ctx || (n && (!res || !bins))) return MTCP_GPU_EINVAL;
+    if (n == 0) return MTCP_GPU_OK;
+    (void)hipSetDevice(ctx->device);
+    Stage &s = ctx->stage[0];
+    int rc = stage_reserve(s, (uint64_t)n * sizeof(uint32_t), n);
+    if (rc != MTCP_GPU_OK) return rc;
+    uint32_t *d_bins = reinterpret_cast<uint32_t *>(s.d_buf);
+    if (!HIP_OK(hipMemcpyAsync(s.d_out, res, (size_t)n * sizeof(mtcp_gpu_result),
+                               hipMemcpyHostToDevice, s.stream)))
+        rc = MTCP_GPU_EIO;
+    if (rc == MTCP_GPU_OK) rc = mtcp_gpu_flow_hash_dev(ctx, s.d_out, n, d_bins, s.stream);
+    if (rc == MTCP_GPU_OK && !HIP_OK(hipMemcpyAsync(bins, d_bins, (size_t)n * sizeof(uint32_t),
+                                                    hipMemcpyDeviceToHost, s.stream)))
+        rc = MTCP_GPU_EIO;
+    if (!HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK) rc = MTCP_GPU_EIO;
+    return rc;
+}
+
+// ---- RSS-friendly address pool -----------------------------
+int mtcp_gpu_rss_queue_map_dev(mtcp_gpu_ctx *ctx, uint32_t saddr_base_h, uint32_t num_addr,
+                               uint32_t daddr_h, uint16_t dport_h, int num_queues,
+                               int endian_check, uint8_t *d_queue, void *stream) {
+    if (!ctx || num_queues < 1 || (num_addr && !d_queue) || ((uintptr_t)d_queue & 3))
+        return MTCP_GPU_EINVAL;
+    if (num_addr == 0) return MTCP_GPU_OK;
+    (void)hipSetDevice(ctx->device);
+    mg::PoolParams pp{};
+    pp.rss_tables = ctx->d_rss_tables;
+    pp.saddr_base_h = saddr_base_h;
+    pp.daddr_h = daddr_h;
+    pp.dport_h = dport_h;
+    pp.nq = (uint32_t)num_queues;
+    pp.endian = endian_check ? 1u : 0u;
+    pp.total = (uint64_t)num_addr * mg::kPorts;
+    const uint64_t quads = (pp.total + 3) / 4;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((quads + mg::kBlock - 1) / mg::kBlock,
+                                                         (uint64_t)ctx->num_cu * 8);
+    hipLaunchKernelGGL(mg::rss_queue_map_kernel, dim3(blocks), dim3(mg::kBlock), 0,
+                       pick(ctx, stream), pp, d_queue);
+    return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
+}
+
+int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues, uint32_t saddr_base,
+                              int num_addr, uint32_t daddr, uint16_t dport, int endian_check,
+                              mtcp_gpu_addr_entry *out, uint32_t max_out, uint32_t *n_found) {
+    if (!ctx || num_queues < 1 || num_addr < 0 || !n_found || (max_out && !out))
+        return MTCP_GPU_EINVAL;
+    *n_found = 0;
+    // addr_pool.c:129 computes num_entry in int: keep the product in range
+    const uint64_t total = (uint64_t)num_addr * mg::kPorts;
+    if (total > (uint64_t)INT32_MAX) return MTCP_GPU_EINVAL;
+    const uint32_t num_entry = (uint32_t)((int)total / num_queues);
+    if (num_addr == 0 || core < 0 || core >= num_queues) return MTCP_GPU_OK;
+    (void)hipSetDevice(ctx->device);
+    const uint32_t nb = (uint32_t)((total + mg::kPoolTile - 1) / mg::kPoolTile);
+    const uint32_t limit = std::min(num_entry, max_out);
+    const uint64_t qbytes = (total + 15) & ~15ull;
+    uint8_t *d_mem = nullptr;
+    const uint64_t out_off = (qbytes + 4ull * (nb + 1) + 7) & ~7ull;     // 8 B aligned entries
+    const uint64_t bytes = out_off + 8ull * std::max(limit, 1u);
+    if (!HIP_OK(hipMalloc(&d_mem, bytes))) return MTCP_GPU_ENOMEM;
+    uint8_t *d_queue = d_mem;
+    uint32_t *d_counts = reinterpret_cast<uint32_t *>(d_mem + qbytes);
+    mtcp_gpu_addr_entry *d_out = reinterpret_cast<mtcp_gpu_addr_entry *>(d_mem + out_off);
+    hipStream_t st = ctx->stream;
+    const uint32_t saddr_base_h = __builtin_bswap32(saddr_base);           // addr_pool.c:150
+    int rc = mtcp_gpu_rss_queue_map_dev(ctx, saddr_base_h, (uint32_t)num_addr,
+                                        __builtin_bswap32(daddr),
+                                        (uint16_t)((dport >> 8) | (dport << 8)), num_queues,
+                                        endian_check, d_queue, st);
+    uint32_t count = 0;
+    if (rc == MTCP_GPU_OK) {
+        hipLaunchKernelGGL(mg::pool_count_kernel, dim3(nb), dim3(mg::kBlock), 0, st, d_queue, total,
+                           (uint32_t)core, d_counts);
+        hipLaunchKernelGGL(mg::pool_scan_kernel, dim3(1), dim3(mg::kBlock), 0, st, d_counts, nb);
+        if (limit)
+            hipLaunchKernelGGL(mg::pool_emit_kernel, dim3(nb), dim3(mg::kBlock), 0, st, d_queue,
+                               total, (uint32_t)core, d_counts, saddr_base_h, limit, d_out);
+        if (!HIP_OK(hipGetLastError()) ||
+            !HIP_OK(hipMemcpyAsync(&count, d_counts + nb, sizeof(count), hipMemcpyDeviceToHost, st)))
+            rc = MTCP_GPU_EIO;
+        if (rc == MTCP_GPU_OK && !HIP_OK(hipStreamSynchronize(st))) rc = MTCP_GPU_EIO;
+        const uint32_t kept = std::min(count, num_entry);
+        const uint32_t copy = std::min(kept, max_out);
+        if (rc == MTCP_GPU_OK && copy &&
+            !HIP_OK(hipMemcpy(out, d_out, (size_t)copy * sizeof(mtcp_gpu_addr_entry),
+                              hipMemcpyDeviceToHost)))
+            rc = MTCP_GPU_EIO;
+        if (rc == MTCP_GPU_OK) *n_found = kept;
+    }
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(d_mem);
     return rc;
 }
 

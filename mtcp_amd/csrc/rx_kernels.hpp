@@ -33,6 +33,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/mtcp_gpu.h"
 
 namespace mg {
@@ -124,6 +126,15 @@ __device__ __forceinline__ uint32_t row_bcast(uint32_t v, int i) {
 #undef MG_NB
 }
 
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N).
+template <int I0, int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I0 < N) {
+        f(std::integral_constant<int, I0>{});
+        static_for<I0 + 1, N>(f);
+    }
+}
+
 // Per-wave LDS, packet-minor ("structure of arrays") so that phase 2, where
 // lane k reads dword i of its own packet, hits 64 distinct banks: dword i of
 // packet k lives at hd[i * kHdStride + k].  Rows 0..27 hold raw chunks 0..6
@@ -165,7 +176,7 @@ struct Trip {
 // ABL (profiling only): 1 = stop after phase 1 (store the chunk sums);
 // 2 = also no LDS header/tail copies; 3 = also no per-chunk range mask.
 template <int MODE, bool RSS, int ABL = 0, int B = 8, bool NT = true, int U = 6, bool PIPE = false,
-          bool PAIR = false>
+          bool PAIR = false, bool UNR = false>
 __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ WaveLds lds[kWavesPerBlock];
@@ -303,6 +314,50 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         const bool has_next = g0 + pass_pkts < kp.n;
 
         // ---------------- phase 1: four frames per wave-instruction ---------
+        if constexpr (UNR) {
+            // The 16 rounds are unrolled, so every row broadcast is a single
+            // constant DPP move.  Round i's first trip streams in buffer X
+            // (i even) or Y (i odd); it was issued one round earlier (round
+            // 0's at the end of the previous pass), and round i issues round
+            // i+1's before consuming its own, so two trips are in flight.
+            // Further trips of a round (frames > 1536 B) load and consume in
+            // place, alongside the next round's first trip.
+            if (!have_pre) {
+                Trip t;
+                enter_round(f, t, 0);
+                issue(t, X);
+            }
+            have_pre = false;
+            uint32_t acc = 0;
+            static_for<0, kWave / 4>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                v4u(&cb)[U] = (i & 1) ? Y : X;
+                v4u(&nb)[U] = (i & 1) ? X : Y;
+                Trip t;
+                enter_round(f, t, i);
+                if constexpr (i + 1 < kWave / 4) {
+                    Trip n;
+                    enter_round(f, n, i + 1);
+                    issue(n, nb);
+                } else if (has_next) {
+                    const Frame fn = decode(g0 + pass_pkts);
+                    Trip n;
+                    enter_round(fn, n, 0);
+                    issue(n, nb);
+                    have_pre = true;
+                }
+                consume(t, cb, acc);
+                while (__ballot(t.c0 + U * kRow < t.nj)) {
+                    t.c0 += U * kRow;
+                    v4u Z[U];
+                    issue(t, Z);
+                    consume(t, Z, acc);
+                }
+                acc = row_sum(acc);
+                if (rlane == kRow - 1) wl.sum[4 * i + (int)row] = acc;
+                acc = 0;
+            });
+        } else
         // Software pipeline: the loads of trip t+1 (or, at the end of the
         // pass, of the next pass's first trip) are issued before trip t is
         // consumed; X and Y alternate.  Every step issues exactly U

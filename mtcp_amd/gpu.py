@@ -14,7 +14,7 @@ import ctypes
 import numpy as np
 
 from ._lib import check, lib
-from ._types import DESC_DTYPE, RESULT_DTYPE
+from ._types import ADDR_ENTRY_DTYPE, DESC_DTYPE, MAX_PORT, MIN_PORT, RESULT_DTYPE
 
 F_RSS = 0x1
 F_RSS_ENDIAN = 0x2
@@ -129,6 +129,44 @@ class Context:
         check(lib().mtcp_gpu_tx_fill(self._h, buf.ctypes.data, buf.nbytes, desc.ctypes.data,
                                      len(desc), off_shift, ctypes.byref(cnt)), "mtcp_gpu_tx_fill")
         return cnt.value
+
+
+    # -- flow-table hash (HashFlow, mtcp/src/tcp_stream.c:56-90) -------------
+    def flow_hash_dev(self, res, n: int, bins, stream=None) -> None:
+        check(lib().mtcp_gpu_flow_hash_dev(self._h, _dptr(res), n, _dptr(bins),
+                                           _stream_handle(stream)), "mtcp_gpu_flow_hash_dev")
+
+    def flow_hash(self, res: np.ndarray) -> np.ndarray:
+        res = np.ascontiguousarray(res, dtype=RESULT_DTYPE)
+        bins = np.zeros(len(res), dtype=np.uint32)
+        check(lib().mtcp_gpu_flow_hash(self._h, res.ctypes.data, len(res), bins.ctypes.data),
+              "mtcp_gpu_flow_hash")
+        return bins
+
+    # -- RSS-friendly address pool (mtcp/src/addr_pool.c:103-180) ------------
+    def rss_queue_map_dev(self, saddr_base_h: int, num_addr: int, daddr_h: int, dport_h: int,
+                          num_queues: int, endian_check: bool, queue, stream=None) -> None:
+        if queue.numel() * queue.element_size() < num_addr * (MAX_PORT - MIN_PORT):
+            raise ValueError("queue buffer too small")
+        check(lib().mtcp_gpu_rss_queue_map_dev(self._h, saddr_base_h, num_addr, daddr_h, dport_h,
+                                               num_queues, int(endian_check), _dptr(queue),
+                                               _stream_handle(stream)),
+              "mtcp_gpu_rss_queue_map_dev")
+
+    def addr_pool_search(self, core: int, num_queues: int, saddr_base: int, num_addr: int,
+                         daddr: int, dport: int, endian_check: bool = True,
+                         max_out: int | None = None) -> np.ndarray:
+        """CreateAddressPoolPerCore's entries for `core` (network-order arguments,
+        as the reference's); returns the ADDR_ENTRY_DTYPE records in pool order."""
+        if max_out is None:
+            max_out = num_addr * (MAX_PORT - MIN_PORT) // max(num_queues, 1)
+        out = np.zeros(max(max_out, 1), dtype=ADDR_ENTRY_DTYPE)
+        found = ctypes.c_uint32(0)
+        check(lib().mtcp_gpu_addr_pool_search(self._h, core, num_queues, saddr_base, num_addr,
+                                              daddr, dport, int(endian_check), out.ctypes.data,
+                                              max_out, ctypes.byref(found)),
+              "mtcp_gpu_addr_pool_search")
+        return out[:min(found.value, max_out)]
 
 
 def host_register(arr: np.ndarray) -> None:

@@ -73,6 +73,11 @@ def lib() -> ctypes.CDLL:
         L.oracle_bench_rx.argtypes = [vp, u64, vp, u32, u32, ctypes.POINTER(RssCfg), vp,
                                       i32, i32]
         L.oracle_bench_rx.restype = ctypes.c_double
+        L.oracle_hash_flow.argtypes = [vp]
+        L.oracle_hash_flow.restype = u32
+        L.oracle_flow_bins.argtypes = [vp, u32, vp]
+        L.oracle_addr_pool_search.argtypes = [vp, i32, i32, u32, i32, u32, u16, i32, vp, u32]
+        L.oracle_addr_pool_search.restype = u32
         _lib = L
     return _lib
 
@@ -129,6 +134,38 @@ def pktgen(buf: np.ndarray, desc: np.ndarray, off_shift: int, seed: int,
            first_index: int = 0) -> None:
     lib().oracle_pktgen(_ptr(buf), buf.nbytes, _ptr(desc), len(desc), off_shift, seed,
                         first_index)
+
+
+ADDR_ENTRY_DTYPE = np.dtype([("saddr", "<u4"), ("sport", "<u2"), ("rsvd", "<u2")])
+
+
+def hash_flow(key12: bytes) -> int:
+    """HashFlow (mtcp/src/tcp_stream.c:56-90) of a 12-byte stream key."""
+    b = (ctypes.c_uint8 * 12).from_buffer_copy(key12)
+    return lib().oracle_hash_flow(ctypes.cast(b, ctypes.c_void_p))
+
+
+def flow_bins(res: np.ndarray) -> np.ndarray:
+    res = np.ascontiguousarray(res, dtype=RESULT_DTYPE)
+    bins = np.zeros(len(res), dtype=np.uint32)
+    lib().oracle_flow_bins(_ptr(res), len(res), _ptr(bins))
+    return bins
+
+
+def addr_pool_search(key: bytes | None, core: int, num_queues: int, saddr_base: int,
+                     num_addr: int, daddr: int, dport: int, endian_check: int = 1,
+                     max_out: int | None = None) -> np.ndarray:
+    """CreateAddressPoolPerCore's search (mtcp/src/addr_pool.c:103-180)."""
+    if max_out is None:
+        max_out = num_addr * 64511 // max(num_queues, 1)
+    out = np.zeros(max(max_out, 1), dtype=ADDR_ENTRY_DTYPE)
+    kb = None
+    if key is not None:
+        kb = (ctypes.c_uint8 * 40).from_buffer_copy(key)
+    n = lib().oracle_addr_pool_search(ctypes.cast(kb, ctypes.c_void_p) if kb else None, core,
+                                      num_queues, saddr_base, num_addr, daddr, dport,
+                                      endian_check, _ptr(out), max_out)
+    return out[:min(n, max_out)]
 
 
 def bench_rx(buf, desc, off_shift, rss, nthreads, reps, out=None) -> float:

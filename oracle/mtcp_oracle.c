@@ -477,3 +477,69 @@ double oracle_bench_rx(const uint8_t *buf, uint64_t buf_len, const mtcp_gpu_desc
     free(args);
     return best;
 }
+
+/* ---- flow-table hash ------------------------------------ */
+/* mtcp/src/tcp_stream.c:77-87: hash += key[i] with key a (signed) char
+ * pointer, so bytes >= 0x80 add a sign-extended negative value. */
+uint32_t oracle_hash_flow(const uint8_t key[12])
+{
+    uint32_t hash = 0;
+    for (int i = 0; i < 12; ++i) {
+        hash += (uint32_t)(int32_t)(int8_t)key[i];
+        hash += hash << 10;
+        hash ^= hash >> 6;
+    }
+    hash += hash << 3;
+    hash ^= hash >> 11;
+    hash += hash << 15;
+    return hash & (MTCP_GPU_NUM_BINS_FLOWS - 1);
+}
+
+void oracle_flow_bins(const mtcp_gpu_result *res, uint32_t n, uint32_t *bins)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        if (res[i].verdict != MTCP_GPU_V_TCP_OK) {
+            bins[i] = MTCP_GPU_FLOW_NONE;
+            continue;
+        }
+        /* tcp_in.c:1180-1183: the local side first */
+        uint8_t key[12];
+        memcpy(key, &res[i].daddr, 4);
+        memcpy(key + 4, &res[i].saddr, 4);
+        memcpy(key + 8, &res[i].dport, 2);
+        memcpy(key + 10, &res[i].sport, 2);
+        bins[i] = oracle_hash_flow(key);
+    }
+}
+
+/* ---- RSS-friendly address pool --------------------------- */
+uint32_t oracle_addr_pool_search(const uint8_t key[40], int core, int num_queues,
+                                 uint32_t saddr_base, int num_addr, uint32_t daddr,
+                                 uint16_t dport, int endian_check,
+                                 mtcp_gpu_addr_entry *out, uint32_t max_out)
+{
+    uint32_t cache[96];
+    oracle_build_key_cache(key ? key : oracle_rss_key_0x05, cache, 96);
+    const uint32_t nports = MTCP_GPU_MAX_PORT - MTCP_GPU_MIN_PORT;
+    /* addr_pool.c:129: int arithmetic, as the reference */
+    const int num_entry = (num_addr * (int)nports) / num_queues;
+    const uint32_t base_h = bswap32(saddr_base), daddr_h = bswap32(daddr);
+    const uint16_t dport_h = bswap16(dport);
+    uint32_t cnt = 0;
+    for (int i = 0; i < num_addr; ++i) {
+        const uint32_t saddr_h = base_h + (uint32_t)i;
+        for (uint32_t j = MTCP_GPU_MIN_PORT; j < MTCP_GPU_MAX_PORT; ++j) {
+            if ((int)cnt >= num_entry) break;                  /* addr_pool.c:160-161 */
+            const int q = oracle_get_rss_cpu_core(cache, daddr_h, saddr_h, dport_h,
+                                                  (uint16_t)j, num_queues, endian_check);
+            if (q != core) continue;
+            if (cnt < max_out) {
+                out[cnt].saddr = bswap32(saddr_h);
+                out[cnt].sport = bswap16((uint16_t)j);
+                out[cnt].rsvd = 0;
+            }
+            cnt++;
+        }
+    }
+    return cnt;
+}

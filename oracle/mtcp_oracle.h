@@ -87,6 +87,33 @@ double oracle_bench_rx(const uint8_t *buf, uint64_t buf_len, const mtcp_gpu_desc
                        uint32_t n, uint32_t off_shift, const oracle_rss_cfg *rss,
                        mtcp_gpu_result *out, int nthreads, int reps);
 
+/*
+ * mtcp/src/tcp_stream.c:56-90 HashFlow (the #else branch: Jenkins
+ * one-at-a-time over the 12 bytes saddr|daddr|sport|dport of a tcp_stream,
+ * tcp_stream.h:163-166, read as x86 signed char), masked to NUM_BINS_FLOWS
+ * (fhash.h:7).
+ */
+uint32_t oracle_hash_flow(const uint8_t key[12]);
+
+/* The flow-table bin of each rx result: HashFlow of the stream key
+ * ProcessTCPPacket looks up (tcp_in.c:1180-1186: saddr = iph->daddr,
+ * sport = tcph->dest, daddr = iph->saddr, dport = tcph->source) for TCP_OK
+ * packets, MTCP_GPU_FLOW_NONE for the rest. */
+void oracle_flow_bins(const mtcp_gpu_result *res, uint32_t n, uint32_t *bins);
+
+/*
+ * mtcp/src/addr_pool.c:103-180 CreateAddressPoolPerCore's search: in
+ * (address, port) order, the (saddr, sport) pairs, network order, whose
+ * GetRSSCPUCore(daddr_h, saddr_h, dport_h, sport_h, nq, endian)
+ * (mtcp/src/rss.c:90-103) is `core`; at most
+ * num_addr * (MAX_PORT - MIN_PORT) / num_queues of them (addr_pool.c:129).
+ * Writes up to max_out entries; returns the number the reference keeps.
+ */
+uint32_t oracle_addr_pool_search(const uint8_t key[40], int core, int num_queues,
+                                 uint32_t saddr_base, int num_addr, uint32_t daddr,
+                                 uint16_t dport, int endian_check,
+                                 mtcp_gpu_addr_entry *out, uint32_t max_out);
+
 #ifdef __cplusplus
 }
 #endif

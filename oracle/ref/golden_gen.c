@@ -275,7 +275,7 @@ int main(int argc, char **argv)
 {
     const char *dir = argc > 1 ? argv[1] : ".";
     mtcp_gpu_result *exp;
-    uint8_t *meta, *work;
+    uint8_t *meta, *work, *fkey;
     uint32_t i, nr;
     char path[4096];
     FILE *man;
@@ -294,6 +294,7 @@ int main(int argc, char **argv)
     /* ---- rx: the reference's verdicts and values ----------------------- */
     exp = (mtcp_gpu_result *)calloc(g_n, sizeof(*exp));
     meta = (uint8_t *)calloc(g_n, 4);
+    fkey = (uint8_t *)calloc(g_n, 12);
     memcpy(work, g_buf, CHUNK_CAP);
     for (i = 0; i < g_n; i++) {
         uint8_t *p = work + g_desc[i].offset;
@@ -306,6 +307,8 @@ int main(int argc, char **argv)
         if (!ub && L >= 34 + 20)
             memcpy(&check_before, p + 14 + 4 * (p[14] & 0xF) + 16, 2);
         br = ref_rx_packet(p, (int)L, &ret, &tcs);
+        if (br == REF_BR_TCP_OK)
+            ref_last_flow_key(fkey + 12 * (size_t)i);   /* tcp_in.c:1180-1186 */
         meta[4 * i + 0] = (uint8_t)ub;
         meta[4 * i + 1] = (uint8_t)br;
         meta[4 * i + 2] = (uint8_t)(ret + 1);
@@ -357,6 +360,7 @@ int main(int argc, char **argv)
     write_file(dir, "rx_desc.bin", g_desc, (size_t)g_n * sizeof(ref_desc_t));
     write_file(dir, "rx_expect.bin", exp, (size_t)g_n * sizeof(*exp));
     write_file(dir, "rx_meta.bin", meta, (size_t)g_n * 4);
+    write_file(dir, "rx_flowkey.bin", fkey, (size_t)g_n * 12);
     fprintf(man, "\"rx_count\": %u,\n\"rx_bytes\": %u,\n\"rss_num_queues\": 8,\n", g_n, g_used);
 
     /* ---- tx fill: zero both check fields, let reference code fill them ---

@@ -25,6 +25,7 @@
 #include "eth_in.h"
 #include "io_module.h"
 #include "ps.h"
+#include "tcp_stream.h"
 
 #include "ref_glue.h"
 
@@ -34,6 +35,7 @@ typedef struct {
     jmp_buf env;
     int released, arp, icmp, tcp_reached, csum_called;
     uint16_t csum_value;
+    uint8_t flow_key[12];            /* s_stream.saddr..dport at StreamHTSearch */
 } probe_t;
 
 static __thread probe_t *g_probe;
@@ -41,7 +43,14 @@ static __thread probe_t *g_probe;
 /* ---- stubs with the reference's prototypes ------------------------------ */
 void *StreamHTSearch(struct hashtable *ht, const void *key)
 {
-    (void)ht; (void)key;
+    /* tcp_in.c:1180-1186: the tcp_stream key HashFlow will hash
+     * (fields saddr, daddr, sport, dport: tcp_stream.h:163-166) */
+    const tcp_stream *s = (const tcp_stream *)key;
+    (void)ht;
+    memcpy(g_probe->flow_key, &s->saddr, 4);
+    memcpy(g_probe->flow_key + 4, &s->daddr, 4);
+    memcpy(g_probe->flow_key + 8, &s->sport, 2);
+    memcpy(g_probe->flow_key + 10, &s->dport, 2);
     longjmp(g_probe->env, 1);        /* tcp_in.c:1186: checksum path passed */
 }
 
@@ -139,14 +148,23 @@ static int ref_run(ref_ctx_t *c, unsigned char *pkt, int len, int *ret_out,
     return REF_BR_UNKNOWN;
 }
 
+static __thread ref_ctx_t *g_ctx1;
+
 int ref_rx_packet(unsigned char *pkt, int len, int *ret_out, uint16_t *tcp_csum)
 {
-    static __thread ref_ctx_t *ctx;
-    if (!ctx) {
-        ctx = (ref_ctx_t *)malloc(sizeof(*ctx));
-        ref_ctx_init(ctx);
+    if (!g_ctx1) {
+        g_ctx1 = (ref_ctx_t *)malloc(sizeof(*g_ctx1));
+        ref_ctx_init(g_ctx1);
     }
-    return ref_run(ctx, pkt, len, ret_out, tcp_csum);
+    return ref_run(g_ctx1, pkt, len, ret_out, tcp_csum);
+}
+
+void ref_last_flow_key(uint8_t key[12])
+{
+    if (g_ctx1)
+        memcpy(key, g_ctx1->probe.flow_key, 12);
+    else
+        memset(key, 0, 12);
 }
 
 uint16_t ref_ip_fast_csum(const void *iph, unsigned int ihl)

@@ -16,6 +16,8 @@ enum {
 typedef struct { uint32_t offset; uint16_t len; uint8_t flags, rsvd; } ref_desc_t;
 
 int      ref_rx_packet(unsigned char *pkt, int len, int *ret_out, uint16_t *tcp_csum);
+/* the stream key StreamHTSearch received for the last TCP_OK ref_rx_packet */
+void     ref_last_flow_key(uint8_t key[12]);
 uint16_t ref_ip_fast_csum(const void *iph, unsigned int ihl);
 uint16_t ref_tcp_calc_checksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t daddr);
 

@@ -1,0 +1,83 @@
+"""the "gpu" io_module backend (mtcp_amd/io_module/gpu_module.c)
+under the rx section of mTCP's RunMainLoop (mtcp/src/core.c:763-777),
+driven by tests/c/rxloop.c over the golden chunk.
+
+CPU: the module compiles against mTCP's own headers (when /root/reference is
+present) and, without a GPU, passes every frame through untouched with
+dev_ioctl answering -1 (mTCP's software checksums, ip_in.c:29-31).
+GPU: get_rptr returns NULL exactly for the frames the reference drops on a
+checksum (ip_in.c:35-36, tcp_in.c:1167-1173), every other frame is served
+byte-identical, and dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers 0.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+GOLD = os.path.join(ROOT, "tests", "golden")
+V_IP_CSUM_BAD, V_TCP_CSUM_BAD = 4, 9
+
+
+def build_rxloop() -> str:
+    subprocess.run(["make", "-s", "tests/c/rxloop"], cwd=ROOT, check=True)
+    return os.path.join(ROOT, "tests", "c", "rxloop")
+
+
+def run_rxloop(tmp_path):
+    exe = build_rxloop()
+    status = tmp_path / "status.bin"
+    p = subprocess.run([exe, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
+                        str(status)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    return json.loads(p.stdout.strip().splitlines()[-1]), np.fromfile(status, dtype=np.uint8)
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "mtcp", "src", "include")),
+                    reason="mTCP headers only in the build container")
+def test_module_compiles_against_mtcp_headers(tmp_path):
+    # the flags of mtcp/src/Makefile.in:20-31 (-Werror included)
+    cmd = ["gcc", "-std=gnu99", "-O3", "-m64", "-Wall", "-Werror", "-fgnu89-inline", "-fcommon",
+           "-DDISABLE_PSIO", "-DDISABLE_NETMAP", "-DDISABLE_DPDK",
+           "-I" + os.path.join(REF, "mtcp", "src", "include"),
+           "-I" + os.path.join(REF, "io_engine", "include"), "-I" + os.path.join(ROOT, "include"),
+           "-c", os.path.join(ROOT, "mtcp_amd", "io_module", "gpu_module.c"),
+           "-o", str(tmp_path / "gpu_module.o")]
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    syms = subprocess.run(["nm", str(tmp_path / "gpu_module.o")], capture_output=True,
+                          text=True).stdout
+    assert " D gpu_module_func" in syms
+
+
+def test_passthrough_without_gpu(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    stats, status = run_rxloop(tmp_path)
+    assert stats["seen"] == stats["frames"] == len(status)
+    assert stats["rx_errors"] == 0 and stats["changed"] == 0
+    assert (status == 1).all()
+    assert stats["ioctl_rx_ip"] == -1 and stats["ioctl_rx_tcp"] == -1
+
+
+@pytest.mark.gpu
+def test_gpu_module_drops_exactly_the_checksum_failures(tmp_path, golden):
+    import oracle
+    stats, status = run_rxloop(tmp_path)
+    v = oracle.rx_chunk(golden.buf, golden.desc, 0)["verdict"]
+    drop = (v == V_IP_CSUM_BAD) | (v == V_TCP_CSUM_BAD)
+    assert stats["seen"] == stats["frames"] == len(golden.desc)
+    assert np.array_equal(status == 0, drop)
+    assert (status[~drop] == 1).all() and stats["changed"] == 0
+    assert stats["rx_errors"] == int(drop.sum()) > 100
+    # on the reference's own verdicts (not ref-UB): the same set
+    ok = golden.meta["ref_ub"] == 0
+    ref_drop = (golden.expect["verdict"] == V_IP_CSUM_BAD) | (golden.expect["verdict"] == V_TCP_CSUM_BAD)
+    assert np.array_equal(drop[ok], ref_drop[ok])
+    assert stats["ioctl_rx_ip"] == 0 and stats["ioctl_rx_tcp"] == 0
+    # bursts were aggregated: fewer GPU launches than PSIO bursts
+    assert stats["rounds"] < stats["inner_bursts"] / 8

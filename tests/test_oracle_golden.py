@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import oracle
-from tests.golden_io import compare_results
+from tests.golden_io import compare_results, pool_case_entries, pool_entries_equal
 
 V_TRUNCATED = 10
 
@@ -148,3 +148,32 @@ def test_pktgen_corruption_rates():
     assert counts[0] > n * 0.99
     assert 20 < counts[9] < 120            # ~1/1024 TCP bit flips
     assert 3 < counts[4] < 40              # ~1/4096 IP header bit flips
+
+
+# ---- HashFlow (mtcp/src/tcp_stream.c:56-90) --------------------
+def test_hash_flow_cases(golden):
+    c = golden.flow_cases
+    got = np.array([oracle.hash_flow(bytes(k)) for k in c["key"]], dtype=np.uint32)
+    assert np.array_equal(got, c["hash"])
+    assert got.max() < 131072            # NUM_BINS_FLOWS mask (fhash.h:7)
+
+
+def test_flow_bins_of_golden_rx(golden):
+    # the reference's own StreamHTSearch key (tcp_in.c:1180-1186), hashed by
+    # the reference's HashFlow, for every golden packet that got that far
+    got = oracle.flow_bins(golden.expect)
+    ok = golden.meta["ref_ub"] == 0
+    assert np.array_equal(got[ok], golden.flow_bins[ok])
+    assert (golden.flow_bins != 0xFFFFFFFF).sum() > 1000
+
+
+# ---- CreateAddressPoolPerCore (mtcp/src/addr_pool.c:103-180) ----
+def test_addr_pool_search_cases(golden):
+    n = 0
+    for c, saddr, sport in pool_case_entries(golden):
+        got = oracle.addr_pool_search(None, int(c["core"]), int(c["nq"]), int(c["saddr_base"]),
+                                      int(c["num_addr"]), int(c["daddr"]), int(c["dport"]),
+                                      int(c["endian"]))
+        assert pool_entries_equal(got, saddr, sport), dict(zip(c.dtype.names, c.tolist()))
+        n += 1
+    assert n == len(golden.pool_cases) >= 8

@@ -54,6 +54,291 @@ __global__ __launch_bounds__(256) void plain_stream(mg::KParams kp) {
     if (acc == 0x12345678u) kp.out[0].saddr = acc;
 }
 
+
+// Ladder from frame_pattern's walk to the rx kernel's phase 1 (C2 layout:
+// frames at a 1536 B stride), one feature at a time.
+//   B     packet<->lane interleave (64 = each wave walks 64 consecutive frames)
+//   DESC  addresses from the descriptors (load, bpermute, row broadcast)
+//   SUMS  0: per-lane accumulator; 1: row sums -> LDS (lane 15, branch)
+//   ST    per-pass stores: 0 none; 1 one dword per 40 B record; 2 one dword
+//         per packet into a dense array; 3 whole 40 B records (8 B pieces)
+//   DBUF  explicit double buffering of the rounds
+template <int B, bool DESC, int SUMS, int ST, bool DBUF>
+__global__ __launch_bounds__(256) void ladder(mg::KParams kp) {
+    using namespace mg;
+    __shared__ uint32_t sums[4][64];
+    __shared__ uint32_t held[ST == 7 ? 4 : 1][ST == 7 ? 32 : 1][64];
+    __shared__ uint32_t rec[ST >= 9 ? 4 : 1][ST == 10 ? 4 * 640 : (ST >= 9 ? 640 : 1)];
+    uint32_t pass_i = 0;
+    uint32_t keep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t lane = threadIdx.x & 63, row = lane >> 4, rl = lane & 15;
+    const uint32_t wib = threadIdx.x >> 6;
+    const uint32_t wave = blockIdx.x * 4 + wib, nw = gridDim.x * 4;
+    const uint64_t base = (uint64_t)(uintptr_t)kp.buf;
+    auto map = [&](uint32_t l) -> uint32_t {
+        return B == 64 ? wave * 64 + l : (l / B) * (nw * B) + wave * B + (l % B);
+    };
+    uint32_t acc = 0;
+    for (uint32_t g0 = 0; g0 < kp.n; g0 += nw * 64) {
+        uint32_t r_lo = 0, r_hi = 0, r_n = 0;
+        const uint32_t k = g0 + map(lane);
+        if constexpr (DESC) {
+            uint64_t p = base;
+            uint32_t nch = 0;
+            if (k < kp.n) {
+                const uint64_t raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
+                p = base + ((uint64_t)(uint32_t)raw << kp.off_shift);
+                const uint32_t L = (uint32_t)(raw >> 32) & 0xFFFFu;
+                nch = (uint32_t)((((p + L + 15) & ~15ull) - (p & ~15ull)) >> 4);
+            }
+            const int src = 4 * (int)rl + (int)row;
+            r_n = shfl32(nch, src);
+            r_lo = shfl32((uint32_t)p, src);
+            r_hi = shfl32((uint32_t)(p >> 32), src);
+        }
+        auto trip = [&](int i, uint64_t &fb, uint32_t &nj) {
+            if constexpr (DESC) {
+                nj = row_bcast(r_n, i);
+                fb = ((uint64_t)row_bcast(r_hi, i) << 32) | row_bcast(r_lo, i);
+            } else {
+                const uint32_t f = g0 + map(4 * i + row);
+                nj = f < kp.n ? 94 : 0;
+                fb = base + (uint64_t)(f < kp.n ? f : 0) * 1536;
+            }
+        };
+        auto issue6 = [&](uint64_t fb, uint32_t nj, v4u (&x)[6]) {
+#pragma unroll
+            for (int u = 0; u < 6; ++u) {
+                const uint32_t c = u * 16 + rl;
+                const uint32_t cc = c < nj ? c : (nj ? nj - 1 : 0u);
+                x[u] = gload_nt(fb + 16ull * cc);
+            }
+        };
+        auto finish = [&](int i, uint32_t nj, const v4u (&x)[6]) {
+            uint32_t a = 0;
+#pragma unroll
+            for (int u = 0; u < 6; ++u) {
+                const uint32_t s4 = halves4(x[u], 0u);
+                a += (u * 16 + rl < nj) ? s4 : 0u;
+            }
+            if constexpr (SUMS == 1) {
+                a = row_sum(a);
+                if (rl == 15) sums[wib][4 * i + row] = a;
+            } else {
+                acc += a;
+            }
+        };
+        if constexpr (DBUF) {
+            v4u X[6], Y[6];
+            uint64_t fb;
+            uint32_t nj;
+            trip(0, fb, nj);
+            issue6(fb, nj, X);
+            static_for<0, 16>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                v4u(&cb)[6] = (i & 1) ? Y : X;
+                v4u(&nb)[6] = (i & 1) ? X : Y;
+                uint64_t cfb, nfb;
+                uint32_t cnj, nnj;
+                trip(i, cfb, cnj);
+                if constexpr (i + 1 < 16) {
+                    trip(i + 1, nfb, nnj);
+                    issue6(nfb, nnj, nb);
+                }
+                finish(i, cnj, cb);
+            });
+        } else {
+            static_for<0, 16>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                uint64_t fb;
+                uint32_t nj;
+                trip(i, fb, nj);
+                v4u x[6];
+                issue6(fb, nj, x);
+                finish(i, nj, x);
+            });
+        }
+        const uint32_t v = SUMS == 1 ? sums[wib][lane] : acc;
+        if (k < kp.n) {
+            if constexpr (ST == 1) kp.out[k].saddr = v;
+            if constexpr (ST == 2) reinterpret_cast<uint32_t *>(kp.out)[k] = v;
+            if constexpr (ST == 3) {
+                uint64_t *o = reinterpret_cast<uint64_t *>(kp.out + k);
+#pragma unroll
+                for (int q = 0; q < 5; ++q) o[q] = (uint64_t)v * (q + 1);
+            }
+            if constexpr (ST == 4) {      // non-temporal stores
+                uint64_t *o = reinterpret_cast<uint64_t *>(kp.out + k);
+#pragma unroll
+                for (int q = 0; q < 5; ++q) __builtin_nontemporal_store((uint64_t)v * (q + 1), o + q);
+            }
+            if constexpr (ST == 5) {      // system-scope relaxed stores (sc0 sc1)
+                uint64_t *o = reinterpret_cast<uint64_t *>(kp.out + k);
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    __hip_atomic_store(o + q, (uint64_t)v * (q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if constexpr (ST == 8) {      // whole records into a per-wave private, L2-resident slot
+                uint64_t *o = reinterpret_cast<uint64_t *>(kp.out + (size_t)wave * 64 + lane);
+#pragma unroll
+                for (int q = 0; q < 5; ++q) o[q] = (uint64_t)v * (q + 1);
+            }
+            if constexpr (ST == 9 || ST == 10 || ST == 11) {   // record -> LDS (SoA-free: AoS)
+                uint32_t *r = &rec[wib][(ST == 10 ? (pass_i & 3) * 640 : 0) + lane * 10];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) r[q] = v + q;
+            }
+            if constexpr (ST == 12) {     // keep the pass's value in a register shift array
+#pragma unroll
+                for (int q = 7; q > 0; --q) keep[q] = keep[q - 1];
+                keep[0] = v;
+            }
+            if constexpr (ST == 7) {      // keep the dword in LDS; written at kernel end
+                held[wib][(g0 / (nw * 64)) & 31][lane] = v;
+            }
+            if constexpr (ST == 6) {      // agent-scope relaxed stores
+                uint64_t *o = reinterpret_cast<uint64_t *>(kp.out + k);
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    __hip_atomic_store(o + q, (uint64_t)v * (q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if constexpr (ST == 9 || ST == 11 || ST == 10) {
+            // coalesced flush of the wave's records: runs of B consecutive packets
+            const bool flush = ST != 10 || (pass_i & 3) == 3 || g0 + nw * 64 >= kp.n;
+            if (flush) {
+                const uint32_t npass = ST == 10 ? (pass_i & 3) + 1 : 1;
+                for (uint32_t pp = 0; pp < npass; ++pp) {
+                    const uint32_t gp = g0 - (npass - 1 - pp) * nw * 64;
+                    const uint32_t *r = &rec[wib][(ST == 10 ? pp * 640 : 0)];
+                    if constexpr (ST == 11) {
+                        // 16 B pieces: 160 per wave-pass, 20 per run of 8 packets
+                        for (uint32_t q = lane; q < 160; q += 64) {
+                            const uint32_t run = q / 20, w = q % 20;
+                            const uint32_t pk = gp + run * (nw * 8) + wave * 8;
+                            uint4 val = make_uint4(r[run * 80 + 4 * w], r[run * 80 + 4 * w + 1],
+                                                   r[run * 80 + 4 * w + 2], r[run * 80 + 4 * w + 3]);
+                            if (pk < kp.n) reinterpret_cast<uint4 *>(kp.out + pk)[w] = val;
+                        }
+                    } else {
+                        for (uint32_t q = lane; q < 320; q += 64) {
+                            const uint32_t run = q / 40, w = q % 40;
+                            const uint32_t pk = gp + run * (nw * 8) + wave * 8;
+                            const uint64_t val = (uint64_t)r[run * 80 + 2 * w] |
+                                                 ((uint64_t)r[run * 80 + 2 * w + 1] << 32);
+                            if (pk < kp.n) reinterpret_cast<uint64_t *>(kp.out + pk)[w] = val;
+                        }
+                    }
+                }
+            }
+        }
+        ++pass_i;
+    }
+    if constexpr (ST == 12) {
+        // pass p's value sits in keep[npass - 1 - p]; whole 40 B records
+        const uint32_t npass = pass_i < 8 ? pass_i : 8;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if ((uint32_t)q < npass) {
+                const uint32_t p = npass - 1 - q;
+                const uint32_t k = p * nw * 64 + map(lane);
+                if (k < kp.n) {
+                    uint64_t *o = reinterpret_cast<uint64_t *>(kp.out + k);
+#pragma unroll
+                    for (int r = 0; r < 5; ++r) o[r] = (uint64_t)keep[q] * (r + 1);
+                }
+            }
+        }
+    }
+    if constexpr (ST == 7) {
+        uint32_t pass = 0;
+        for (uint32_t g0 = 0; g0 < kp.n && pass < 32; g0 += nw * 64, ++pass) {
+            const uint32_t k = g0 + map(lane);
+            if (k < kp.n) kp.out[k].saddr = held[wib][pass][lane];
+        }
+    }
+    if (ST == 0 && acc == 0x12345678u) kp.out[0].saddr = acc;
+}
+
+
+// Writer-wave split: waves 0-3 of a 320-thread workgroup stream frames (as
+// lad_B8_desc) and leave one 40 B record per packet in LDS; wave 4 stores
+// the previous pass's records while the readers stream the next one, so no
+// reader ever waits behind a store.  One LDS-only barrier per pass.
+__global__ __launch_bounds__(320) void ww_ladder(mg::KParams kp) {
+    using namespace mg;
+    __shared__ uint32_t rec[2][4][640];
+    const uint32_t lane = threadIdx.x & 63, row = lane >> 4, rl = lane & 15;
+    const uint32_t wib = threadIdx.x >> 6;
+    const bool writer = wib == 4;
+    const uint32_t nw = gridDim.x * 4;
+    const uint32_t wave = blockIdx.x * 4 + (writer ? 0 : wib);
+    const uint64_t base = (uint64_t)(uintptr_t)kp.buf;
+    auto map = [&](uint32_t l) -> uint32_t { return (l / 8) * (nw * 8) + wave * 8 + (l % 8); };
+    const uint32_t pass_pkts = nw * 64;
+    const uint32_t npass = (kp.n + pass_pkts - 1) / pass_pkts;
+    for (uint32_t ps = 0; ps <= npass; ++ps) {
+        const uint32_t g0 = ps * pass_pkts;
+        if (!writer && ps < npass) {
+            uint32_t r_lo = 0, r_hi = 0, r_n = 0;
+            const uint32_t k = g0 + map(lane);
+            {
+                uint64_t p = base;
+                uint32_t nch = 0;
+                if (k < kp.n) {
+                    const uint64_t raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
+                    p = base + ((uint64_t)(uint32_t)raw << kp.off_shift);
+                    const uint32_t L = (uint32_t)(raw >> 32) & 0xFFFFu;
+                    nch = (uint32_t)((((p + L + 15) & ~15ull) - (p & ~15ull)) >> 4);
+                }
+                const int src = 4 * (int)rl + (int)row;
+                r_n = shfl32(nch, src);
+                r_lo = shfl32((uint32_t)p, src);
+                r_hi = shfl32((uint32_t)(p >> 32), src);
+            }
+            uint32_t acc = 0;
+            static_for<0, 16>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                const uint32_t nj = row_bcast(r_n, i);
+                const uint64_t fb = ((uint64_t)row_bcast(r_hi, i) << 32) | row_bcast(r_lo, i);
+                v4u x[6];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    const uint32_t c = u * 16 + rl;
+                    const uint32_t cc = c < nj ? c : (nj ? nj - 1 : 0u);
+                    x[u] = gload_nt(fb + 16ull * cc);
+                }
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    const uint32_t s4 = halves4(x[u], 0u);
+                    acc += (u * 16 + rl < nj) ? s4 : 0u;
+                }
+            });
+            uint32_t *r = &rec[ps & 1][wib][lane * 10];
+#pragma unroll
+            for (int q = 0; q < 10; ++q) r[q] = acc + q;
+        }
+        if (writer && ps > 0) {
+            // pass ps-1: reader wave w's lanes l own packets map_w(l); runs of 8
+            const uint32_t gp = (ps - 1) * pass_pkts;
+            for (uint32_t w = 0; w < 4; ++w) {
+                const uint32_t *r = rec[(ps - 1) & 1][w];
+                const uint32_t ww_wave = blockIdx.x * 4 + w;
+                for (uint32_t q = lane; q < 320; q += 64) {
+                    const uint32_t run = q / 40, d = q % 40;
+                    const uint32_t pk = gp + run * (nw * 8) + ww_wave * 8;
+                    const uint64_t val = (uint64_t)r[run * 80 + 2 * d] |
+                                         ((uint64_t)r[run * 80 + 2 * d + 1] << 32);
+                    if (pk < kp.n) reinterpret_cast<uint64_t *>(kp.out + pk)[d] = val;
+                }
+            }
+        }
+        // LDS-only barrier: no vmcnt wait, so neither the readers' prefetch nor
+        // the writer's stores are drained here
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+}
+
 struct Variant { const char *name; kfn fn; uint32_t blocks_per_cu; };
 
 static uint64_t mix(uint64_t z) {
@@ -118,12 +403,26 @@ int main(int argc, char **argv) {
     using namespace mg;
     if (rss) {
         vs.push_back({"rss_U6_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false>, 4});
+        vs.push_back({"rss_unr_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, true>, 2});
+        vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     } else {
         vs.push_back({"U6_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false>, 2});
-        vs.push_back({"abl1_p1only", rx_kernel<kRxChunk, false, 1, 8, true, 6, false>, 2});
-        vs.push_back({"abl2_nolds", rx_kernel<kRxChunk, false, 2, 8, true, 6, false>, 2});
-        vs.push_back({"abl3_nomask", rx_kernel<kRxChunk, false, 3, 8, true, 6, false>, 2});
-        vs.push_back({"abl3_nomask_cu3", rx_kernel<kRxChunk, false, 3, 8, true, 6, false>, 3});
+        vs.push_back({"unr_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, true>, 2});
+        if (strcmp(cfg, "c2") == 0) {
+            vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
+            vs.push_back({"lad_B8_desc_sums", ladder<8, true, 1, 0, false>, 2});
+            vs.push_back({"lad_B8_desc_st1", ladder<8, true, 0, 1, false>, 2});
+            vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
+            vs.push_back({"lad_B8_desc_st3", ladder<8, true, 0, 3, false>, 2});
+            vs.push_back({"lad_B64_desc_st3", ladder<64, true, 0, 3, false>, 2});
+            vs.push_back({"lad_B8_desc_st3_dbuf", ladder<8, true, 0, 3, true>, 2});
+            vs.push_back({"lad_B8_desc_st7_atend", ladder<8, true, 0, 7, false>, 2});
+            vs.push_back({"lad_B8_desc_st9_coal8", ladder<8, true, 0, 9, false>, 2});
+            vs.push_back({"lad_B8_desc_st12_regs_atend", ladder<8, true, 0, 12, false>, 2});
+            vs.push_back({"lad_B8_desc_st11_coal16", ladder<8, true, 0, 11, false>, 2});
+            vs.push_back({"lad_B8_desc_st10_flush4", ladder<8, true, 0, 10, false>, 2});
+            vs.push_back({"lad_B8_desc_st8_private", ladder<8, true, 0, 8, false>, 2});
+        }
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     }
     if (single) vs.resize(1);
@@ -139,15 +438,17 @@ int main(int argc, char **argv) {
             if (blocks > cus * vs[v].blocks_per_cu) blocks = cus * vs[v].blocks_per_cu;
             kp.out = v == 0 ? d_ref : d_out;
             CK(hipMemset(kp.out, 0, n * sizeof(mtcp_gpu_result)));
-            hipLaunchKernelGGL(vs[v].fn, dim3(blocks), dim3(256), 0, 0, kp);
+            const uint32_t threads = strncmp(vs[v].name, "ww_", 3) == 0 ? 320 : 256;
+            hipLaunchKernelGGL(vs[v].fn, dim3(blocks), dim3(threads), 0, 0, kp);
             CK(hipEventRecord(a));
-            for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(blocks), dim3(256), 0, 0, kp);
+            for (int i = 0; i < reps; ++i)
+                hipLaunchKernelGGL(vs[v].fn, dim3(blocks), dim3(threads), 0, 0, kp);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float t;
             CK(hipEventElapsedTime(&t, a, b));
             ms[v].push_back(t / reps);
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "plain")) {
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && strncmp(vs[v].name, "ww_", 3) != 0) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
