@@ -175,8 +175,13 @@ struct Trip {
 // that, round by round, the whole grid streams one compact window of frames.
 // ABL (profiling only): 1 = stop after phase 1 (store the chunk sums);
 // 2 = also no LDS header/tail copies; 3 = also no per-chunk range mask.
+// DEFER (rx modes): results of up to DEFER passes wait in registers and are
+// stored together when the buffer is full and at the end, instead of after
+// every pass.  Stores interleaved with the frame stream cost far more HBM
+// time than their bytes (tools/rx_variants ladder: 40 B/packet written per
+// pass +45 us on C2, written at the end +18 us); DEFER 0 stores per pass.
 template <int MODE, bool RSS, int ABL = 0, int B = 8, bool NT = true, int U = 6, bool PIPE = false,
-          bool PAIR = false, bool UNR = false>
+          bool PAIR = false, bool UNR = false, int DEFER = 8>
 __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ WaveLds lds[kWavesPerBlock];
@@ -296,6 +301,28 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 d[0] = x[u].x; d[kHdStride] = x[u].y;
                 d[2 * kHdStride] = x[u].z; d[3 * kHdStride] = x[u].w;
             }
+        }
+    };
+
+    constexpr int kDefer = MODE == kTxChunk ? 0 : DEFER;
+    uint32_t keep[kDefer > 0 ? kDefer : 1][10];   // keep[q]: the record of q passes ago
+    uint32_t held = 0;                            // passes in keep[] (wave-uniform)
+    uint32_t last_g0 = 0;                         // pass base of keep[0]
+    // store the held records (lane k's record of pass last_g0 - q*pass_pkts)
+    auto flush = [&]() {
+        if constexpr (kDefer > 0) {
+#pragma unroll
+            for (int q = 0; q < kDefer; ++q) {
+                if ((uint32_t)q < held) {
+                    const uint32_t rec = last_g0 - (uint32_t)q * pass_pkts + lane_off;
+                    if (rec < kp.n) {
+                        uint2 *o = reinterpret_cast<uint2 *>(kp.out + rec);
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) o[i] = make_uint2(keep[q][2 * i], keep[q][2 * i + 1]);
+                    }
+                }
+            }
+            held = 0;
         }
     };
 
@@ -648,6 +675,24 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 q16[(T + 16) >> 1] = (uint16_t)tcp_csum;              // tcph->check (tcp_out.c:329)
                 if (kp.fill_count) atomicAdd(kp.fill_count, 1u);
             }
+        } else if constexpr (kDefer > 0) {
+            if (held == (uint32_t)kDefer) flush();
+#pragma unroll
+            for (int q = kDefer - 1; q > 0; --q)
+#pragma unroll
+                for (int i = 0; i < 10; ++i) keep[q][i] = keep[q - 1][i];
+            keep[0][0] = saddr;
+            keep[0][1] = daddr;
+            keep[0][2] = ports;
+            keep[0][3] = seq;
+            keep[0][4] = ack;
+            keep[0][5] = window | (ip_len << 16);
+            keep[0][6] = ip_csum | (tcp_csum << 16);
+            keep[0][7] = rss_hash;
+            keep[0][8] = payload_len | (ihl_doff << 16) | (flags << 24);
+            keep[0][9] = verdict | (rss_queue << 8) | (eth_type << 16);
+            last_g0 = g0;
+            ++held;
         } else {
             // stage the 64 records (2560 B) in this wave's LDS, then store
             // them as 8-byte pieces: lanes of one run of B packets write one
@@ -668,6 +713,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
             }
         }
     }
+    flush();
 }
 
 }  // namespace mg

@@ -403,10 +403,14 @@ int main(int argc, char **argv) {
     using namespace mg;
     if (rss) {
         vs.push_back({"rss_U6_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false>, 4});
+        vs.push_back({"rss_U6_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false>, 2});
+        vs.push_back({"rss_defer0_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, false, 0>, 4});
         vs.push_back({"rss_unr_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, true>, 2});
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     } else {
         vs.push_back({"U6_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false>, 2});
+        vs.push_back({"defer0_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, false, 0>, 2});
+        vs.push_back({"defer4_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, false, 4>, 2});
         vs.push_back({"unr_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, true>, 2});
         if (strcmp(cfg, "c2") == 0) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
