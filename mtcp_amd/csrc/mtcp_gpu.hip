@@ -94,15 +94,33 @@ uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
     return std::max(1u, std::min(blocks, cap));
 }
 
+// Phase-1 schedule by the chunk's average slot size: with mostly large
+// frames (C2 1500 B, C5 9000 B) the rolled trip loop streams best; with many
+// small frames (C3: half 64 B) a round carries fewer bytes and the fully
+// unrolled, double-buffered rounds win (tools/rx_variants: C2 246 vs 254 us,
+// C3 164 vs 145 us).  Pointer bursts have no chunk size: rolled.
+constexpr uint64_t kUnrollBelowSlotBytes = 1024;
+
+template <int MODE, bool RSS, int UNR>
+void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
+    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, 0, 8, true, 6, false, false, UNR>), grid, block, 0,
+                       st, kp);
+}
+
 template <int MODE>
 int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     if (kp.n == 0) return MTCP_GPU_OK;
     const dim3 grid(grid_for(ctx, kp.n)), block(mg::kBlock);
     const bool rss = MODE != mg::kTxChunk && (ctx->flags & MTCP_GPU_F_RSS);
-    if (rss)
-        hipLaunchKernelGGL((mg::rx_kernel<MODE, true>), grid, block, 0, st, kp);
+    const bool small = MODE == mg::kRxChunk && kp.buf_len / kp.n < kUnrollBelowSlotBytes;
+    if (rss && small)
+        launch_one<MODE, true, 1>(grid, block, st, kp);
+    else if (rss)
+        launch_one<MODE, true, 0>(grid, block, st, kp);
+    else if (small)
+        launch_one<MODE, false, 1>(grid, block, st, kp);
     else
-        hipLaunchKernelGGL((mg::rx_kernel<MODE, false>), grid, block, 0, st, kp);
+        launch_one<MODE, false, 0>(grid, block, st, kp);
     return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
 

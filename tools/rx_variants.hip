@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void ladder(mg::KParams kp) {
 #pragma unroll
                 for (int q = 0; q < 10; ++q) r[q] = v + q;
             }
-            if constexpr (ST == 12) {     // keep the pass's value in a register shift array
+            if constexpr (ST >= 12) {     // keep the pass's value in a register shift array
 #pragma unroll
                 for (int q = 7; q > 0; --q) keep[q] = keep[q - 1];
                 keep[0] = v;
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void ladder(mg::KParams kp) {
         }
         ++pass_i;
     }
-    if constexpr (ST == 12) {
+    if constexpr (ST == 12 || ST == 14) {
         // pass p's value sits in keep[npass - 1 - p]; whole 40 B records
         const uint32_t npass = pass_i < 8 ? pass_i : 8;
 #pragma unroll
@@ -245,7 +245,42 @@ __global__ __launch_bounds__(256) void ladder(mg::KParams kp) {
                 if (k < kp.n) {
                     uint64_t *o = reinterpret_cast<uint64_t *>(kp.out + k);
 #pragma unroll
-                    for (int r = 0; r < 5; ++r) o[r] = (uint64_t)keep[q] * (r + 1);
+                    for (int r = 0; r < 5; ++r) {
+                        if constexpr (ST == 14)
+                            __builtin_nontemporal_store((uint64_t)keep[q] * (r + 1), o + r);
+                        else
+                            o[r] = (uint64_t)keep[q] * (r + 1);
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (ST == 13 || ST == 15) {
+        // coalesced: the wave's records of one pass through LDS, runs of 8 packets
+        const uint32_t npass = pass_i < 8 ? pass_i : 8;
+        uint32_t *r = rec[wib];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if ((uint32_t)q < npass) {
+                const uint32_t gp = (npass - 1 - q) * nw * 64;
+#pragma unroll
+                for (int d = 0; d < 10; ++d) r[lane * 10 + d] = keep[q] + d;
+                if constexpr (ST == 13) {
+                    for (uint32_t qq = lane; qq < 320; qq += 64) {
+                        const uint32_t run = qq / 40, w = qq % 40;
+                        const uint32_t pk = gp + run * (nw * 8) + wave * 8;
+                        const uint64_t val = (uint64_t)r[run * 80 + 2 * w] |
+                                             ((uint64_t)r[run * 80 + 2 * w + 1] << 32);
+                        if (pk < kp.n) reinterpret_cast<uint64_t *>(kp.out + pk)[w] = val;
+                    }
+                } else {
+                    for (uint32_t qq = lane; qq < 160; qq += 64) {
+                        const uint32_t run = qq / 20, w = qq % 20;
+                        const uint32_t pk = gp + run * (nw * 8) + wave * 8;
+                        const uint4 val = make_uint4(r[run * 80 + 4 * w], r[run * 80 + 4 * w + 1],
+                                                     r[run * 80 + 4 * w + 2], r[run * 80 + 4 * w + 3]);
+                        if (pk < kp.n) reinterpret_cast<uint4 *>(kp.out + pk)[w] = val;
+                    }
                 }
             }
         }
@@ -404,27 +439,25 @@ int main(int argc, char **argv) {
     if (rss) {
         vs.push_back({"rss_U6_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false>, 4});
         vs.push_back({"rss_U6_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false>, 2});
-        vs.push_back({"rss_defer0_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, false, 0>, 4});
-        vs.push_back({"rss_unr_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, true>, 2});
+        vs.push_back({"rss_defer0_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 0, 0>, 4});
+        vs.push_back({"rss_unr_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 1>, 2});
+        vs.push_back({"rss_pair_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 2>, 2});
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     } else {
         vs.push_back({"U6_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false>, 2});
-        vs.push_back({"defer0_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, false, 0>, 2});
-        vs.push_back({"defer4_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, false, 4>, 2});
-        vs.push_back({"unr_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, true>, 2});
+        vs.push_back({"defer0_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 0, 0>, 2});
+        vs.push_back({"defer4_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 0, 4>, 2});
+        vs.push_back({"unr_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 1>, 2});
+        vs.push_back({"pair_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 2>, 2});
         if (strcmp(cfg, "c2") == 0) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
-            vs.push_back({"lad_B8_desc_sums", ladder<8, true, 1, 0, false>, 2});
-            vs.push_back({"lad_B8_desc_st1", ladder<8, true, 0, 1, false>, 2});
             vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
             vs.push_back({"lad_B8_desc_st3", ladder<8, true, 0, 3, false>, 2});
-            vs.push_back({"lad_B64_desc_st3", ladder<64, true, 0, 3, false>, 2});
-            vs.push_back({"lad_B8_desc_st3_dbuf", ladder<8, true, 0, 3, true>, 2});
             vs.push_back({"lad_B8_desc_st7_atend", ladder<8, true, 0, 7, false>, 2});
-            vs.push_back({"lad_B8_desc_st9_coal8", ladder<8, true, 0, 9, false>, 2});
             vs.push_back({"lad_B8_desc_st12_regs_atend", ladder<8, true, 0, 12, false>, 2});
-            vs.push_back({"lad_B8_desc_st11_coal16", ladder<8, true, 0, 11, false>, 2});
-            vs.push_back({"lad_B8_desc_st10_flush4", ladder<8, true, 0, 10, false>, 2});
+            vs.push_back({"lad_B8_desc_st13_regs_coal8", ladder<8, true, 0, 13, false>, 2});
+            vs.push_back({"lad_B8_desc_st14_regs_nt", ladder<8, true, 0, 14, false>, 2});
+            vs.push_back({"lad_B8_desc_st15_regs_coal16", ladder<8, true, 0, 15, false>, 2});
             vs.push_back({"lad_B8_desc_st8_private", ladder<8, true, 0, 8, false>, 2});
         }
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
