@@ -346,6 +346,21 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         }
     };
 
+    // hold this pass's record (flushing first when the buffer is full)
+    auto push = [&](const uint32_t (&r)[10], uint32_t g0) {
+        if constexpr (kDefer > 0) {
+            if (held == (uint32_t)kDefer) flush();
+#pragma unroll
+            for (int q = kDefer - 1; q > 0; --q)
+#pragma unroll
+                for (int i = 0; i < 10; ++i) keep[q][i] = keep[q - 1][i];
+#pragma unroll
+            for (int i = 0; i < 10; ++i) keep[0][i] = r[i];
+            last_g0 = g0;
+            ++held;
+        }
+    };
+
     fetch(0);
     v4u X[U], Y[U];
     Trip pre;                    // next pass's first trip, already issued into X
@@ -418,6 +433,35 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 finish_round(cur, Y);
                 cur = nxt;
                 nxt = n2;
+            }
+        } else if constexpr (UNR == 3) {
+            // The 16 rounds unrolled (constant DPP broadcasts) but single-
+            // buffered: each round's loads are issued, then consumed, like
+            // the read-only walk of tools/rx_variants (lad_B8_desc); only the
+            // next pass's first trip is issued before phase 2.
+            uint32_t acc = 0;
+            static_for<0, kWave / 4>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                Trip t;
+                enter_round(f, t, i);
+                if (i > 0 || !have_pre) issue(t, X);
+                consume(t, X, acc);
+                while (__ballot(t.c0 + U * kRow < t.nj)) {
+                    t.c0 += U * kRow;
+                    issue(t, X);
+                    consume(t, X, acc);
+                }
+                acc = row_sum(acc);
+                if (rlane == kRow - 1) wl.sum[4 * i + (int)row] = acc;
+                acc = 0;
+            });
+            have_pre = false;
+            if (has_next) {
+                const Frame fn = decode(g0 + pass_pkts);
+                Trip n;
+                enter_round(fn, n, 0);
+                issue(n, X);
+                have_pre = true;
             }
         } else if constexpr (UNR == 1) {
             // The 16 rounds are unrolled, so every row broadcast is a single
@@ -575,7 +619,12 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         }
 
         if constexpr (ABL >= 1) {
-            if (live) kp.out[k].saddr = wl.sum[lane];
+            if constexpr (kDefer > 0) {
+                const uint32_t r[10] = {wl.sum[lane], 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                push(r, g0);
+            } else if (live) {
+                kp.out[k].saddr = wl.sum[lane];
+            }
             continue;
         }
         // ---------------- phase 2: per-lane parse and finish ---------------
@@ -754,23 +803,11 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 if (kp.fill_count) atomicAdd(kp.fill_count, 1u);
             }
         } else if constexpr (kDefer > 0) {
-            if (held == (uint32_t)kDefer) flush();
-#pragma unroll
-            for (int q = kDefer - 1; q > 0; --q)
-#pragma unroll
-                for (int i = 0; i < 10; ++i) keep[q][i] = keep[q - 1][i];
-            keep[0][0] = saddr;
-            keep[0][1] = daddr;
-            keep[0][2] = ports;
-            keep[0][3] = seq;
-            keep[0][4] = ack;
-            keep[0][5] = window | (ip_len << 16);
-            keep[0][6] = ip_csum | (tcp_csum << 16);
-            keep[0][7] = rss_hash;
-            keep[0][8] = payload_len | (ihl_doff << 16) | (flags << 24);
-            keep[0][9] = verdict | (rss_queue << 8) | (eth_type << 16);
-            last_g0 = g0;
-            ++held;
+            const uint32_t r[10] = {saddr, daddr, ports, seq, ack, window | (ip_len << 16),
+                                    ip_csum | (tcp_csum << 16), rss_hash,
+                                    payload_len | (ihl_doff << 16) | (flags << 24),
+                                    verdict | (rss_queue << 8) | (eth_type << 16)};
+            push(r, g0);
         } else {
             // stage the 64 records (2560 B) in this wave's LDS, then store
             // them as 8-byte pieces: lanes of one run of B packets write one
