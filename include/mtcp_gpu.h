@@ -141,10 +141,16 @@ typedef struct mtcp_gpu_result {
     uint16_t window;      /* 20 ntohs(tcph->window)     tcp_in.c:1149          */
     uint16_t ip_len;      /* 22 ntohs(iph->tot_len)     ip_in.c:21             */
     uint16_t ip_csum;     /* 24 ip_fast_csum(iph, ihl)  ip_in.c:35 (0 = good)  */
-    uint16_t tcp_csum;    /* 26 TCPCalcChecksum(...)    tcp_in.c:1165 (0 = good) */
+    uint16_t tcp_csum;    /* 26 TCPCalcChecksum(...)    tcp_in.c:1165 (0 = good);
+                                 verdict ICMP: ICMPChecksum(iph + 4*ihl, ip_len - 4*ihl)
+                                 (icmp.c:18-42, checked at icmp.c:94) when the datagram
+                                 lies inside the frame, else 0; an odd ICMP length makes
+                                 the reference read an uninitialised byte (icmp.c:31-33):
+                                 the missing high byte is taken as 0 here       */
     uint32_t rss_hash;    /* 28 GetRSSHash(ntohl(saddr), ntohl(daddr),
                                            ntohs(sport), ntohs(dport))         */
-    uint16_t payload_len; /* 32 ip_len - 4*(ihl+doff)   tcp_in.c:1144          */
+    uint16_t payload_len; /* 32 ip_len - 4*(ihl+doff)   tcp_in.c:1144
+                                 (ICMP: the ICMP length ip_len - 4*ihl, >= 0)     */
     uint8_t  ihl_doff;    /* 34 ihl | doff << 4                                */
     uint8_t  tcp_flags;   /* 35 FIN 0x01 SYN 0x02 RST 0x04 PSH 0x08 ACK 0x10 URG 0x20 */
     uint8_t  verdict;     /* 36 enum mtcp_gpu_verdict                          */

@@ -640,7 +640,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         uint32_t saddr = 0, daddr = 0, ports = 0, seq = 0, ack = 0, window = 0, flags = 0;
         uint32_t payload_len = 0, rss_hash = 0, rss_queue = 0;
         uint32_t tcp_len = 0, T = 0, s_ip = 0, tcheck = 0, tcp_csum = 0;
-        bool need_sum = false;
+        bool need_sum = false, icmp = false;
         const uint32_t d0 = h[3];                 // bytes 12..15
         if (desc_ok) {
             verdict = MTCP_GPU_V_TRUNCATED;
@@ -678,6 +678,18 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                             verdict = MTCP_GPU_V_IP_VERSION;               // ip_in.c:47-50
                         } else if (proto == 1) {
                             verdict = MTCP_GPU_V_ICMP;
+                            // ICMPChecksum(icmph, ip_len - 4*ihl) (icmp.c:18-42),
+                            // the echo-request check of icmp.c:94, when the
+                            // datagram lies inside the frame; a negative length
+                            // skips the loop: ~0
+                            if (14 + ip_len <= L) {
+                                if (ip_len >= 4 * ihl) {
+                                    icmp = need_sum = true;
+                                    tcp_len = payload_len = ip_len - 4 * ihl;
+                                } else {
+                                    tcp_csum = 0xFFFFu;
+                                }
+                            }
                         } else if (proto != 6) {
                             verdict = MTCP_GPU_V_IP_PROTO_OTHER;           // ip_in.c:57-59
                         } else if (L >= T + 16) {
@@ -785,12 +797,14 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
             }
             uint32_t s = wl.sum[lane] - s_out;                     // exact segment sum
             if (MODE == kTxChunk) s -= tcheck;                     // computed with check = 0
-            s += (saddr & 0xFFFFu) + (saddr >> 16);                // tcp_util.c:179-182
-            s += (daddr & 0xFFFFu) + (daddr >> 16);
-            s += bswap16(tcp_len);
-            s += 0x0600u;                                          // htons(IPPROTO_TCP)
-            tcp_csum = fold_csum(s);
-            if (MODE != kTxChunk)
+            if (!icmp) {
+                s += (saddr & 0xFFFFu) + (saddr >> 16);            // tcp_util.c:179-182
+                s += (daddr & 0xFFFFu) + (daddr >> 16);
+                s += bswap16(tcp_len);
+                s += 0x0600u;                                      // htons(IPPROTO_TCP)
+            }
+            tcp_csum = fold_csum(s);                               // icmp.c:36-38 folds alike
+            if (MODE != kTxChunk && !icmp)
                 verdict = tcp_csum ? MTCP_GPU_V_TCP_CSUM_BAD : MTCP_GPU_V_TCP_OK;   // tcp_in.c:1167-1173
         }
 

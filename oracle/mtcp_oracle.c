@@ -174,6 +174,25 @@ void oracle_rss_cfg_init(oracle_rss_cfg *cfg, const uint8_t key[40], int num_que
  * byte it checks that the byte lies inside the frame; where the reference
  * would read past `len` (undefined behaviour) the verdict is TRUNCATED.
  */
+/* mtcp/src/icmp.c:18-42 ICMPChecksum.  A negative len skips the loop (the
+ * assert is compiled out): ~0.  An odd len reads the last byte into the low
+ * half of an uninitialised u16 (icmp.c:31-33, undefined); the high half is
+ * taken as 0 here. */
+uint16_t oracle_icmp_checksum(const uint8_t *icmph, int len)
+{
+    uint32_t sum = 0;
+    while (len > 1) {
+        sum += ld16(icmph);
+        icmph += 2;
+        len -= 2;
+    }
+    if (len == 1)
+        sum += *icmph;
+    sum = (sum >> 16) + (sum & 0xffff);
+    sum += (sum >> 16);
+    return (uint16_t)~sum;
+}
+
 int oracle_rx_packet(const uint8_t *pkt, uint32_t len, const oracle_rss_cfg *rss,
                      mtcp_gpu_result *r)
 {
@@ -207,8 +226,16 @@ int oracle_rx_packet(const uint8_t *pkt, uint32_t len, const oracle_rss_cfg *rss
         VERDICT(MTCP_GPU_V_IP_VERSION);
     NEED(24);
     proto = pkt[23];                                 /* ip_in.c:52 */
-    if (proto == 1)
+    if (proto == 1) {
+        /* ProcessICMPECHORequest's check (icmp.c:94): ICMPChecksum over
+         * ip_len - 4*ihl bytes from iph + 4*ihl, when they lie in the frame */
+        if (14 + ip_len <= len) {
+            int ilen = (int)ip_len - (int)(ihl << 2);
+            r->tcp_csum = oracle_icmp_checksum(pkt + 14 + 4 * ihl, ilen);
+            r->payload_len = (uint16_t)(ilen > 0 ? ilen : 0);
+        }
         VERDICT(MTCP_GPU_V_ICMP);
+    }
     if (proto != 6)
         VERDICT(MTCP_GPU_V_IP_PROTO_OTHER);
 

@@ -29,6 +29,9 @@ uint16_t oracle_ip_fast_csum(const void *iph, unsigned int ihl);
 uint16_t oracle_tcp_calc_checksum(const uint16_t *buf, uint16_t len,
                                   uint32_t saddr, uint32_t daddr);
 
+/* mtcp/src/icmp.c:18-42 (ICMPChecksum; odd len: high byte taken as 0). */
+uint16_t oracle_icmp_checksum(const uint8_t *icmph, int len);
+
 /* util/rss.c:13-105 BuildKeyCache with the key as a parameter. */
 void oracle_build_key_cache(const uint8_t key[40], uint32_t *cache, int cache_len);
 

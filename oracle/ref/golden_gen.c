@@ -219,6 +219,53 @@ static void build_edge_cases(void)
     }
 }
 
+/* ICMP (protocol 1) frames whose ICMP checksum the reference checks for an
+ * echo request (icmp.c:94): checksum filled by the reference's ICMPChecksum,
+ * even and odd ICMP lengths, several ihl, corrupted copies, a datagram
+ * shorter than its header (negative length) and one longer than the frame. */
+static void build_icmp_cases(void)
+{
+    static const uint32_t ihls[3] = {5, 6, 15};
+    uint32_t k, j;
+    for (k = 0; k < 48; k++) {
+        uint32_t ihl = ihls[k % 3], L = 60 + rndn(1400), T = 14 + 4 * ihl;
+        int32_t ipl = (int32_t)(L - 14) - (int32_t)rndn(8);
+        uint8_t *p;
+        uint16_t c;
+        if ((int32_t)(4 * ihl) + 8 > ipl) ipl = (int32_t)(4 * ihl) + 8;
+        for (j = 0; j < 2; j++) {
+            p = build_tcp(L, ihl, 5, ipl, 0);
+            p[23] = 1;
+            p[T] = 8;                                  /* ICMP_ECHO */
+            p[T + 1] = 0;
+            p[24] = p[25] = 0;
+            c = ref_ip_fast_csum(p + 14, ihl);
+            memcpy(p + 24, &c, 2);
+            p[T + 2] = p[T + 3] = 0;
+            c = ref_icmp_checksum(p + T, ipl - (int32_t)(4 * ihl));
+            memcpy(p + T + 2, &c, 2);
+            if (j == 1)
+                flip_bit(p, T, 14 + (uint32_t)ipl);
+        }
+    }
+    for (k = 0; k < 4; k++) {                          /* tot_len < 4*ihl: length < 0 */
+        uint8_t *p = build_tcp(120, 15, 5, 20 + 8 * k, 0);
+        uint16_t c;
+        p[23] = 1;
+        p[24] = p[25] = 0;
+        c = ref_ip_fast_csum(p + 14, 15);
+        memcpy(p + 24, &c, 2);
+    }
+    for (k = 0; k < 4; k++) {                          /* datagram past the frame */
+        uint8_t *p = build_tcp(100 + 20 * k, 5, 5, 100 + 20 * k, 0);
+        uint16_t c;
+        p[23] = 1;
+        p[24] = p[25] = 0;
+        c = ref_ip_fast_csum(p + 14, 5);
+        memcpy(p + 24, &c, 2);
+    }
+}
+
 /* Samples of each BASELINE.json config, produced by the synthetic generator. */
 static void build_config_samples(FILE *man)
 {
@@ -287,6 +334,7 @@ int main(int argc, char **argv)
     fprintf(man, "{\n\"generator\": \"oracle/ref/golden_gen.c (reference code from /root/reference)\",\n");
 
     build_edge_cases();
+    build_icmp_cases();
     fprintf(man, "\"edge_count\": %u,\n\"samples\": [\n", g_n);
     build_config_samples(man);
     fprintf(man, "\n],\n");
@@ -332,6 +380,16 @@ int main(int argc, char **argv)
         if (br == REF_BR_IP_SHORT)
             continue;
         r->ip_csum = ref_ip_fast_csum(p + 14, ihl);
+        if (br == REF_BR_ICMP && 14u + r->ip_len <= L) {
+            /* the echo-request check of icmp.c:94 over ip_len - 4*ihl bytes */
+            int ilen = (int)r->ip_len - (int)(4 * ihl);
+            if (ilen > 0 && (ilen & 1)) {
+                meta[4 * i + 0] = 2;          /* icmp.c:31-33 reads an uninitialised byte */
+            } else {
+                r->tcp_csum = ref_icmp_checksum(p + 14 + 4 * ihl, ilen);
+                r->payload_len = (uint16_t)(ilen > 0 ? ilen : 0);
+            }
+        }
         if (br == REF_BR_IP_CSUM_BAD || br == REF_BR_IP_VERSION || br == REF_BR_ICMP ||
             br == REF_BR_IP_PROTO_OTHER)
             continue;

@@ -21,6 +21,9 @@ void     ref_last_flow_key(uint8_t key[12]);
 uint16_t ref_ip_fast_csum(const void *iph, unsigned int ihl);
 uint16_t ref_tcp_calc_checksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t daddr);
 
+/* mtcp/src/icmp.c:18-42 ICMPChecksum (static; reached via ref_icmp.c) */
+uint16_t ref_icmp_checksum(const uint8_t *icmph, int len);
+
 /* util/rss.c (key 0x05, compiled as shipped) */
 uint32_t ref_util_rss_hash(uint32_t sip, uint32_t dip, uint16_t sp, uint16_t dp);
 int      ref_util_rss_core(uint32_t sip, uint32_t dip, uint16_t sp, uint16_t dp, int nq);

@@ -19,6 +19,7 @@ STUB(AddtoTimewaitList)
 STUB(CreateTCPStream)
 STUB(DestroyTCPStream)
 STUB(EnqueueACK)
+STUB(IPOutputStandalone)
 STUB(ListenerHTSearch)
 STUB(RBInit)
 STUB(RBPut)

@@ -177,3 +177,18 @@ def test_addr_pool_search_cases(golden):
         assert pool_entries_equal(got, saddr, sport), dict(zip(c.dtype.names, c.tolist()))
         n += 1
     assert n == len(golden.pool_cases) >= 8
+
+
+# ---- ICMPChecksum (mtcp/src/icmp.c:18-42) ---------------------
+def test_icmp_checksum_cases(golden):
+    e, m = golden.expect, golden.meta
+    icmp = (e["verdict"] == 6) & (m["ref_ub"] == 0)
+    got = oracle.rx_chunk(golden.buf, golden.desc, 0)
+    assert np.array_equal(got["tcp_csum"][icmp], e["tcp_csum"][icmp])
+    assert np.array_equal(got["payload_len"][icmp], e["payload_len"][icmp])
+    # echo requests with the reference's checksum (0), corrupted copies,
+    # negative lengths (~0) and odd lengths (reference UB, flagged 2)
+    assert ((e["tcp_csum"] == 0) & icmp & (e["payload_len"] > 0)).sum() >= 20
+    assert ((e["tcp_csum"] != 0) & icmp).sum() >= 20
+    assert ((e["tcp_csum"] == 0xFFFF) & icmp).sum() >= 4
+    assert ((m["ref_ub"] == 2) & (e["verdict"] == 6)).sum() >= 10
