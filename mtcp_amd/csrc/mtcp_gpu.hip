@@ -96,9 +96,10 @@ uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
 
 // Phase-1 schedule by the chunk's average slot size: with mostly large
 // frames (C2 1500 B, C5 9000 B) the rolled trip loop streams best; with many
-// small frames (C3: half 64 B) a round carries fewer bytes and the fully
-// unrolled, double-buffered rounds win (tools/rx_variants: C2 246 vs 254 us,
-// C3 164 vs 145 us).  Pointer bursts have no chunk size: rolled.
+// small frames (C3: half 64 B) the size-sorted rounds win — large frames four
+// per round, double-buffered, small ones sixteen per round
+// (tools/rx_variants, one box: C2 rolled 244 / sorted 248 us; C3 rolled 164,
+// unrolled 145, sorted 141 us).  Pointer bursts have no chunk size: rolled.
 constexpr uint64_t kUnrollBelowSlotBytes = 1024;
 
 template <int MODE, bool RSS, int UNR>
@@ -114,11 +115,11 @@ int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     const bool rss = MODE != mg::kTxChunk && (ctx->flags & MTCP_GPU_F_RSS);
     const bool small = MODE == mg::kRxChunk && kp.buf_len / kp.n < kUnrollBelowSlotBytes;
     if (rss && small)
-        launch_one<MODE, true, 1>(grid, block, st, kp);
+        launch_one<MODE, true, 4>(grid, block, st, kp);
     else if (rss)
         launch_one<MODE, true, 0>(grid, block, st, kp);
     else if (small)
-        launch_one<MODE, false, 1>(grid, block, st, kp);
+        launch_one<MODE, false, 4>(grid, block, st, kp);
     else
         launch_one<MODE, false, 0>(grid, block, st, kp);
     return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;

@@ -145,7 +145,8 @@ constexpr int kHdRows = 4 * kSlotChunks;   // 32
 constexpr int kHdStride = kWave + 1;       // 65 dwords
 struct WaveLds {
     uint32_t hd[kHdRows * kHdStride];
-    uint32_t sum[kWave];
+    uint32_t sum[kWave + 1];       // [kWave]: scratch for rows without a frame
+    uint4 info[kWave];             // size-sorted schedule: {p16 lo, p16 hi, nch, owner}
 };
 
 // A lane's frame: address, length, descriptor validity, and its chunk range
@@ -167,6 +168,7 @@ struct Trip {
     int i;
     uint32_t c0, nj;
     uint64_t base;
+    uint32_t col;     // the frame's owner lane = its column in WaveLds (kWave: scratch)
 };
 
 // Packet <-> lane mapping, in passes of 64*W packets (W = waves in the grid):
@@ -259,6 +261,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     auto enter_round = [&](const Frame &f, Trip &t, int ii) {
         t.i = ii;
         t.c0 = 0;
+        t.col = 4 * (uint32_t)ii + row;
         t.nj = row_bcast(f.r_nch, ii);
         t.base = ((uint64_t)row_bcast(f.r_hi, ii) << 32) | row_bcast(f.r_lo, ii);
     };
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         }
     };
     auto consume = [&](const Trip &t, const v4u (&x)[U], uint32_t &acc) {
-        const int j = 4 * t.i + (int)row;
+        const uint32_t j = t.col;
         if (ABL < 2 && t.c0 == 0 && rlane < kSlotChunks - 1) {       // raw chunks 0..6
             uint32_t *d = wl.hd + 4 * rlane * kHdStride + j;
             d[0] = x[0].x; d[kHdStride] = x[0].y;
@@ -304,6 +307,70 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 d[0] = x[u].x; d[kHdStride] = x[u].y;
                 d[2 * kHdStride] = x[u].z; d[3 * kHdStride] = x[u].w;
             }
+        }
+    };
+
+    // ---- size-sorted schedule (UNR == 4) ---------------------------------
+    constexpr uint32_t kSmallChunks = 4;        // <= 64 B on the 16 B grid
+    constexpr uint32_t kQuads = kWave / 4;      // small frames per round
+    uint32_t pre_nL = 0, pre_nS = 0;            // class counts of the pre-issued pass
+    // rank the wave's frames by class and publish {base, chunks, owner}
+    auto prepare = [&](const Frame &fr, uint32_t &nL, uint32_t &nS) {
+        const bool big = fr.nch > kSmallChunks, sml = fr.nch != 0 && !big;
+        const uint64_t mb = __ballot(big), ms = __ballot(sml);
+        nL = (uint32_t)__popcll(mb);
+        nS = (uint32_t)__popcll(ms);
+        const uint64_t below = (1ull << lane) - 1;
+        const uint4 e = make_uint4((uint32_t)fr.p16, (uint32_t)(fr.p16 >> 32), fr.nch, lane);
+        if (big) wl.info[__popcll(mb & below)] = e;
+        if (sml) wl.info[kWave - 1 - __popcll(ms & below)] = e;
+    };
+    auto big_trip = [&](uint32_t nL, uint32_t ii, Trip &t) {
+        const uint32_t r = 4 * ii + row;
+        t.i = (int)ii;
+        t.c0 = 0;
+        t.nj = 0;
+        t.base = safe;
+        t.col = kWave;                            // scratch column
+        if (r < nL) {
+            const uint4 e = wl.info[r];
+            t.base = ((uint64_t)e.y << 32) | e.x;
+            t.nj = e.z;
+            t.col = e.w;
+        }
+    };
+    auto small_trip = [&](uint32_t nS, uint32_t ii, Trip &t) {
+        const uint32_t r = kQuads * ii + (lane >> 2);
+        t.i = (int)ii;
+        t.c0 = 0;
+        t.nj = 0;
+        t.base = safe;
+        t.col = kWave;
+        if (r < nS) {
+            const uint4 e = wl.info[kWave - 1 - r];
+            t.base = ((uint64_t)e.y << 32) | e.x;
+            t.nj = e.z;
+            t.col = e.w;
+        }
+    };
+    auto small_load = [&](const Trip &t) -> v4u {
+        const uint32_t q = lane & 3;
+        const uint32_t cc = q < t.nj ? q : (t.nj ? t.nj - 1 : 0u);
+        return NT ? gload_nt(t.base + 16ull * cc) : gload(t.base + 16ull * cc);
+    };
+    auto small_finish = [&](const Trip &t, const v4u &v) {
+        const uint32_t q = lane & 3;
+        uint32_t s4 = q < t.nj ? halves4(v, 0u) : 0u;
+        s4 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s4, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+        s4 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s4, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+        if (q == 0) wl.sum[t.col] = s4;
+        if (q < t.nj) {                                              // raw chunk q
+            uint32_t *d = wl.hd + 4 * q * kHdStride + t.col;
+            d[0] = v.x; d[kHdStride] = v.y; d[2 * kHdStride] = v.z; d[3 * kHdStride] = v.w;
+        }
+        if (q + 1 == t.nj) {                                         // last chunk
+            uint32_t *d = wl.hd + 4 * (kSlotChunks - 1) * kHdStride + t.col;
+            d[0] = v.x; d[kHdStride] = v.y; d[2 * kHdStride] = v.z; d[3 * kHdStride] = v.w;
         }
     };
 
@@ -376,7 +443,76 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         const bool has_next = g0 + pass_pkts < kp.n;
 
         // ---------------- phase 1: four frames per wave-instruction ---------
-        if constexpr (UNR == 2) {
+        if constexpr (UNR == 4) {
+            // Size-sorted rounds.  The wave's frames are ranked by class:
+            // large (> kSmallChunks chunks) frames stream four per round as
+            // above (a 16-lane row each, U loads per lane), small ones
+            // sixteen per round (a 4-lane quad each, one load per lane);
+            // empty ones are skipped.  A mix of 64 B and 1500 B frames then
+            // needs ~10 round trips per pass instead of 16, and no round
+            // waits on a large frame with mostly small ones.  The rank ->
+            // frame table (base, chunk count, owner lane) lives in LDS; each
+            // lane reads its row's / quad's entry (LDS broadcast).  Large
+            // rounds are double-buffered (X/Y).
+            uint32_t nL, nS;
+            if (!have_pre) prepare(f, nL, nS);
+            else nL = pre_nL, nS = pre_nS;
+            const uint32_t RL = (nL + 3) / 4, RS = (nS + kQuads - 1) / kQuads;
+            uint32_t acc = 0;
+            auto finish_big = [&](Trip &t, const v4u (&cb)[U]) {
+                consume(t, cb, acc);
+                while (__ballot(t.c0 + U * kRow < t.nj)) {
+                    t.c0 += U * kRow;
+                    v4u Z[U];
+                    issue(t, Z);
+                    consume(t, Z, acc);
+                }
+                acc = row_sum(acc);
+                if (rlane == kRow - 1) wl.sum[t.col] = acc;
+                acc = 0;
+            };
+            if (RL > 0) {
+                Trip cur, nxt;
+                if (have_pre) {
+                    cur = pre;
+                } else {
+                    big_trip(nL, 0, cur);
+                    issue(cur, X);
+                }
+                for (uint32_t i = 0; i < RL; i += 2) {
+                    if (i + 1 < RL) {                 // round i+1 goes out into Y
+                        big_trip(nL, i + 1, nxt);
+                        issue(nxt, Y);
+                    }
+                    finish_big(cur, X);
+                    if (i + 1 >= RL) break;
+                    if (i + 2 < RL) {                 // round i+2 into X
+                        big_trip(nL, i + 2, cur);
+                        issue(cur, X);
+                    }
+                    finish_big(nxt, Y);
+                }
+            }
+            have_pre = false;
+            // small rounds, two at a time (two loads in flight per lane)
+            for (uint32_t i = 0; i < RS; i += 2) {
+                Trip a, b;
+                small_trip(nS, i, a);
+                small_trip(nS, i + 1, b);
+                const v4u va = small_load(a), vb = small_load(b);
+                small_finish(a, va);
+                small_finish(b, vb);
+            }
+            if (has_next) {                           // the next pass's first large round
+                const Frame fn = decode(g0 + pass_pkts);
+                prepare(fn, pre_nL, pre_nS);
+                if (pre_nL) {
+                    big_trip(pre_nL, 0, pre);
+                    issue(pre, X);
+                    have_pre = true;
+                }
+            }
+        } else if constexpr (UNR == 2) {
             // Rounds in pairs: round i (even) streams in X, i+1 in Y.  The
             // trip of round i+1 is issued before round i is consumed, and the
             // trip info of round i+2 (frame 4(i+2)+row's base and chunk count,
@@ -386,6 +522,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 const int src = 4 * ii + (int)row;                 // the frame's owner lane
                 t.i = ii;
                 t.c0 = 0;
+                t.col = (uint32_t)src;
                 t.nj = shfl32(fr.nch, src);
                 t.base = ((uint64_t)shfl32((uint32_t)(fr.p16 >> 32), src) << 32) |
                          shfl32((uint32_t)fr.p16, src);

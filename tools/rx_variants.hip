@@ -443,6 +443,7 @@ int main(int argc, char **argv) {
         vs.push_back({"rss_unr_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 1>, 2});
         vs.push_back({"rss_pair_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 2>, 2});
         vs.push_back({"rss_unr1buf_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 3>, 2});
+        vs.push_back({"rss_sorted_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 4>, 2});
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     } else {
         vs.push_back({"U6_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false>, 2});
@@ -451,6 +452,7 @@ int main(int argc, char **argv) {
         vs.push_back({"unr_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 1>, 2});
         vs.push_back({"pair_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 2>, 2});
         vs.push_back({"unr1buf_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 3>, 2});
+        vs.push_back({"sorted_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 4>, 2});
         if (strcmp(cfg, "c2") == 0) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
             vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
