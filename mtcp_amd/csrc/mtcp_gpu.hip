@@ -95,11 +95,13 @@ uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
 }
 
 // Phase-1 schedule by the chunk's average slot size: with mostly large
-// frames (C2 1500 B, C5 9000 B) the rolled trip loop streams best; with many
-// small frames (C3: half 64 B) the size-sorted rounds win — large frames four
-// per round, double-buffered, small ones sixteen per round
-// (tools/rx_variants, one box: C2 rolled 244 / sorted 248 us; C3 rolled 164,
-// unrolled 145, sorted 141 us).  Pointer bursts have no chunk size: rolled.
+// frames (C2 1500 B, C5 9000 B) the 16 rounds unrolled and single-buffered
+// (UNR 3) stream best; with many small frames (C3: half 64 B) the size-sorted
+// rounds win — large frames four per round, double-buffered, small ones
+// sixteen per round (tools/rx_variants, in-process A/B, four boxes: C2
+// unrolled 240.9-243.1 / rolled 244.2-246.0 / sorted 248-250 us; C5 unrolled
+// and rolled equal, 683-686 us; C3 rolled 164, unrolled 145, sorted 141 us).
+// Pointer bursts have no chunk size: unrolled.
 constexpr uint64_t kUnrollBelowSlotBytes = 1024;
 
 template <int MODE, bool RSS, int UNR>
@@ -117,11 +119,11 @@ int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     if (rss && small)
         launch_one<MODE, true, 4>(grid, block, st, kp);
     else if (rss)
-        launch_one<MODE, true, 0>(grid, block, st, kp);
+        launch_one<MODE, true, 3>(grid, block, st, kp);
     else if (small)
         launch_one<MODE, false, 4>(grid, block, st, kp);
     else
-        launch_one<MODE, false, 0>(grid, block, st, kp);
+        launch_one<MODE, false, 3>(grid, block, st, kp);
     return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
 

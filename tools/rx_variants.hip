@@ -444,6 +444,10 @@ int main(int argc, char **argv) {
         vs.push_back({"rss_pair_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 2>, 2});
         vs.push_back({"rss_unr1buf_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 3>, 2});
         vs.push_back({"rss_sorted_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 4>, 2});
+        vs.push_back({"abl1_rss_sorted_cu2", rx_kernel<kRxChunk, true, 1, 8, true, 6, false, false, 4>, 2});
+        vs.push_back({"abl2_rss_sorted_cu2", rx_kernel<kRxChunk, true, 2, 8, true, 6, false, false, 4>, 2});
+        vs.push_back({"abl1_rss_sorted_nostore_cu2", rx_kernel<kRxChunk, true, 1, 8, true, 6, false, false, 4, 0>, 2});
+        vs.push_back({"norss_sorted_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 4>, 2});
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     } else {
         vs.push_back({"U6_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false>, 2});
@@ -489,7 +493,7 @@ int main(int argc, char **argv) {
             float t;
             CK(hipEventElapsedTime(&t, a, b));
             ms[v].push_back(t / reps);
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && strncmp(vs[v].name, "ww_", 3) != 0) {
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "norss") && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && strncmp(vs[v].name, "ww_", 3) != 0) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
