@@ -101,13 +101,38 @@ uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
 // sixteen per round (tools/rx_variants, in-process A/B, four boxes: C2
 // unrolled 240.9-243.1 / rolled 244.2-246.0 / sorted 248-250 us; C5 unrolled
 // and rolled equal, 683-686 us; C3 rolled 164, unrolled 145, sorted 141 us).
+// The sorted schedule issues the first two small rounds together with the
+// pre-issued first large round, through L2 (UNR 6): a 64 B frame shares its
+// 128 B line with a neighbour's edge that another round streams, and the
+// early temporal load lets that round hit it (C3 140.7 -> 134.3 us).
 // Pointer bursts have no chunk size: unrolled.
+// Frames longer than one trip (1536 B) are streamed from the start of their
+// first 128 B line (rx_kernel LALIGN) so that no trip boundary splits a line:
+// C5's 9024 B slots put every other frame off the line grid, and without it
+// 2.4 % of the chunk is fetched twice (PMC FETCH_SIZE 4.887 -> 4.768 GB per
+// launch; 688.6 vs 690.7 us).  Chunks of <= 1536 B slots skip the bookkeeping.
 constexpr uint64_t kUnrollBelowSlotBytes = 1024;
+constexpr uint64_t kLineAlignAboveSlotBytes = 1536;
 
-template <int MODE, bool RSS, int UNR>
+template <int MODE, bool RSS, int UNR, bool LALIGN>
 void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
-    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, 0, 8, true, 6, false, false, UNR>), grid, block, 0,
-                       st, kp);
+    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, 0, 8, true, 6, false, false, UNR, 8, LALIGN>), grid,
+                       block, 0, st, kp);
+}
+
+template <int MODE, bool RSS>
+void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
+    if constexpr (MODE == mg::kRxPtrs) {
+        launch_one<MODE, RSS, 3, true>(grid, block, st, kp);      // pointers: any frame size
+    } else {
+        const uint64_t slot = kp.buf_len / kp.n;
+        if (slot < kUnrollBelowSlotBytes)
+            launch_one<MODE, RSS, 6, false>(grid, block, st, kp);
+        else if (slot > kLineAlignAboveSlotBytes)
+            launch_one<MODE, RSS, 3, true>(grid, block, st, kp);
+        else
+            launch_one<MODE, RSS, 3, false>(grid, block, st, kp);
+    }
 }
 
 template <int MODE>
@@ -115,15 +140,10 @@ int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     if (kp.n == 0) return MTCP_GPU_OK;
     const dim3 grid(grid_for(ctx, kp.n)), block(mg::kBlock);
     const bool rss = MODE != mg::kTxChunk && (ctx->flags & MTCP_GPU_F_RSS);
-    const bool small = MODE == mg::kRxChunk && kp.buf_len / kp.n < kUnrollBelowSlotBytes;
-    if (rss && small)
-        launch_one<MODE, true, 4>(grid, block, st, kp);
-    else if (rss)
-        launch_one<MODE, true, 3>(grid, block, st, kp);
-    else if (small)
-        launch_one<MODE, false, 4>(grid, block, st, kp);
+    if (rss)
+        launch_sched<MODE, true>(grid, block, st, kp);
     else
-        launch_one<MODE, false, 3>(grid, block, st, kp);
+        launch_sched<MODE, false>(grid, block, st, kp);
     return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
 

@@ -169,6 +169,7 @@ struct Trip {
     uint32_t c0, nj;
     uint64_t base;
     uint32_t col;     // the frame's owner lane = its column in WaveLds (kWave: scratch)
+    uint32_t skip = 0;  // LALIGN: chunks before the frame at the start of the first trip
 };
 
 // Packet <-> lane mapping, in passes of 64*W packets (W = waves in the grid):
@@ -187,8 +188,8 @@ struct Trip {
 // rounds fully unrolled (constant DPP broadcasts); 2 = a loop over pairs of
 // rounds whose trip info comes from ds_bpermute one round ahead.
 template <int MODE, bool RSS, int ABL = 0, int B = 8, bool NT = true, int U = 6, bool PIPE = false,
-          bool PAIR = false, int UNR = 0, int DEFER = 8>
-__global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
+          bool PAIR = false, int UNR = 0, int DEFER = 8, bool LALIGN = true>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ WaveLds lds[kWavesPerBlock];
     if constexpr (RSS) {
@@ -259,12 +260,29 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     };
 
     // ---------------- phase 1 building blocks -----------------------------
+    // LALIGN: a frame that needs more than one trip is streamed from the
+    // start of its first 128 B line: the trip's base moves back by the
+    // `skip` = (p16 & 127) / 16 chunks before the frame (same line, same page;
+    // masked out of the sum), so that every later trip starts on a line.  A
+    // trip boundary inside a line would fetch that line twice, once per trip
+    // (C5: 9024 B slots put every other frame off the line grid).
+    auto line_align = [&](Trip &t) {
+        t.skip = 0;
+        if constexpr (LALIGN) {
+            if (t.nj > (uint32_t)(U * kRow)) {
+                t.skip = (uint32_t)((t.base & 127) >> 4);
+                t.base -= 16ull * t.skip;
+                t.nj += t.skip;
+            }
+        }
+    };
     auto enter_round = [&](const Frame &f, Trip &t, int ii) {
         t.i = ii;
-        t.c0 = 0;
         t.col = 4 * (uint32_t)ii + row;
         t.nj = row_bcast(f.r_nch, ii);
         t.base = ((uint64_t)row_bcast(f.r_hi, ii) << 32) | row_bcast(f.r_lo, ii);
+        t.c0 = 0;
+        line_align(t);
     };
     // next trip with work; false (nj = 0, base kept valid) when the pass is done
     auto advance = [&](const Frame &f, Trip &t) -> bool {
@@ -293,8 +311,9 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     };
     auto consume = [&](const Trip &t, const v4u (&x)[U], uint32_t &acc) {
         const uint32_t j = t.col;
-        if (ABL < 2 && t.c0 == 0 && rlane < kSlotChunks - 1) {       // raw chunks 0..6
-            uint32_t *d = wl.hd + 4 * rlane * kHdStride + j;
+        const uint32_t c_hd = rlane - t.skip;                        // frame chunk of x[0]
+        if (ABL < 2 && t.c0 == 0 && c_hd < kSlotChunks - 1) {        // first trip: raw chunks 0..6
+            uint32_t *d = wl.hd + 4 * c_hd * kHdStride + j;
             d[0] = x[0].x; d[kHdStride] = x[0].y;
             d[2 * kHdStride] = x[0].z; d[3 * kHdStride] = x[0].w;
         }
@@ -302,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         for (int u = 0; u < U; ++u) {
             const uint32_t c = t.c0 + u * kRow + rlane;
             const uint32_t s = halves4(x[u], 0u);
-            acc += (ABL >= 3 || c < t.nj) ? s : 0u;
+            acc += (ABL >= 3 || c - t.skip < t.nj - t.skip) ? s : 0u;   // skip <= c < nj
             if (ABL < 2 && c == t.nj - 1) {                            // last chunk
                 uint32_t *d = wl.hd + 4 * (kSlotChunks - 1) * kHdStride + j;
                 d[0] = x[u].x; d[kHdStride] = x[u].y;
@@ -330,6 +349,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         const uint32_t r = 4 * ii + row;
         t.i = (int)ii;
         t.c0 = 0;
+        t.skip = 0;
         t.nj = 0;
         t.base = safe;
         t.col = kWave;                            // scratch column
@@ -338,12 +358,14 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
             t.base = ((uint64_t)e.y << 32) | e.x;
             t.nj = e.z;
             t.col = e.w;
+            line_align(t);
         }
     };
     auto small_trip = [&](uint32_t nS, uint32_t ii, Trip &t) {
         const uint32_t r = kQuads * ii + (lane >> 2);
         t.i = (int)ii;
         t.c0 = 0;
+        t.skip = 0;
         t.nj = 0;
         t.base = safe;
         t.col = kWave;
@@ -357,7 +379,9 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     auto small_load = [&](const Trip &t) -> v4u {
         const uint32_t q = lane & 3;
         const uint32_t cc = q < t.nj ? q : (t.nj ? t.nj - 1 : 0u);
-        return NT ? gload_nt(t.base + 16ull * cc) : gload(t.base + 16ull * cc);
+        // UNR 5: small frames load through L2 normally (their 128 B line is
+        // shared with a neighbour's edge, streamed in another round)
+        return NT && UNR < 5 ? gload_nt(t.base + 16ull * cc) : gload(t.base + 16ull * cc);
     };
     auto small_finish = [&](const Trip &t, const v4u &v) {
         const uint32_t q = lane & 3;
@@ -433,6 +457,9 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
     v4u X[U], Y[U];
     Trip pre;                    // next pass's first trip, already issued into X
     bool have_pre = false;
+    Trip sa, sb;                 // UNR >= 5: the first two small rounds
+    v4u va, vb;
+    bool have_pre_small = false; // UNR 6: already issued into va, vb
     for (uint32_t g0 = 0; g0 < kp.n; g0 += pass_pkts) {
         const Frame f = decode(g0);
         if (!__ballot(f.live)) break;
@@ -444,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
         const bool has_next = g0 + pass_pkts < kp.n;
 
         // ---------------- phase 1: four frames per wave-instruction ---------
-        if constexpr (UNR == 4) {
+        if constexpr (UNR >= 4) {
             // Size-sorted rounds.  The wave's frames are ranked by class:
             // large (> kSmallChunks chunks) frames stream four per round as
             // above (a 16-lane row each, U loads per lane), small ones
@@ -472,6 +499,28 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 if (rlane == kRow - 1) wl.sum[t.col] = acc;
                 acc = 0;
             };
+            // UNR 5: the first two small rounds go out with the first large
+            // round, before the large frames around them stream.  UNR 6:
+            // they go out even earlier, with the pre-issued first large round
+            // at the end of the previous pass (below).
+            if constexpr (UNR >= 5) {
+                if (have_pre_small) {
+                    // issued at the end of the previous pass
+                } else if (RL > 0 && !have_pre) {
+                    Trip t0;
+                    big_trip(nL, 0, t0);
+                    issue(t0, X);
+                    pre = t0;
+                    have_pre = true;
+                }
+                if (!have_pre_small) {
+                    small_trip(nS, 0, sa);
+                    small_trip(nS, 1, sb);
+                    va = small_load(sa);
+                    vb = small_load(sb);
+                }
+                have_pre_small = false;
+            }
             if (RL > 0) {
                 Trip cur, nxt;
                 if (have_pre) {
@@ -495,8 +544,16 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 }
             }
             have_pre = false;
+            uint32_t s0 = 0;
+            if constexpr (UNR >= 5) {
+                if (RS > 0) {
+                    small_finish(sa, va);
+                    small_finish(sb, vb);
+                }
+                s0 = 2;
+            }
             // small rounds, two at a time (two loads in flight per lane)
-            for (uint32_t i = 0; i < RS; i += 2) {
+            for (uint32_t i = s0; i < RS; i += 2) {
                 Trip a, b;
                 small_trip(nS, i, a);
                 small_trip(nS, i + 1, b);
@@ -507,6 +564,13 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
             if (has_next) {                           // the next pass's first large round
                 const Frame fn = decode(g0 + pass_pkts);
                 prepare(fn, pre_nL, pre_nS);
+                if constexpr (UNR == 6) {
+                    small_trip(pre_nS, 0, sa);
+                    small_trip(pre_nS, 1, sb);
+                    va = small_load(sa);
+                    vb = small_load(sb);
+                    have_pre_small = true;
+                }
                 if (pre_nL) {
                     big_trip(pre_nL, 0, pre);
                     issue(pre, X);
@@ -523,6 +587,7 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(KParams kp) {
                 const int src = 4 * ii + (int)row;                 // the frame's owner lane
                 t.i = ii;
                 t.c0 = 0;
+                t.skip = 0;
                 t.col = (uint32_t)src;
                 t.nj = shfl32(fr.nch, src);
                 t.base = ((uint64_t)shfl32((uint32_t)(fr.p16 >> 32), src) << 32) |

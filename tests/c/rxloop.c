@@ -12,12 +12,14 @@
  *   rxloop CHUNK DESC OUT
  *     CHUNK  frame bytes; DESC mtcp_gpu_desc records (byte offsets)
  *     OUT    one byte per frame: 0 NULL, 1 served intact, 2 served but changed
- * Prints one JSON line with the counters.  Built with the test doubles in
+ * Prints one JSON line with the counters and the wall time of the rx loop
+ * (tools/io_path_bench.py turns that into the io_module path's rate).  Built with the test doubles in
  * tests/c/mtcp_double (two fields of mtcp_thread_context, io_module_func).
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "mtcp.h"
 #include "io_module.h"
@@ -100,6 +102,9 @@ int main(int argc, char **argv)
     uint64_t rx_packets = 0, rx_errors = 0, changed = 0;
     int rounds = 0, ioctl_ip = -2, ioctl_tcp = -2;
     uint32_t seen = 0;
+    uint64_t frame_bytes = 0;
+    struct timespec t0, t1;
+    double secs;
     FILE *out;
 
     if (argc < 4) { fprintf(stderr, "usage: rxloop CHUNK DESC OUT\n"); return 1; }
@@ -112,6 +117,7 @@ int main(int argc, char **argv)
     gpu_module_func.load_module();
     gpu_module_func.init_handle(&ctx);
     gpu_module_func.link_devices(&ctx);
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     for (;;) {                                        /* core.c:763-777 */
         int32_t recv_cnt = gpu_module_func.recv_pkts(&ctx, 0), i;
         if (recv_cnt <= 0)
@@ -137,15 +143,20 @@ int main(int argc, char **argv)
         }
         seen += (uint32_t)recv_cnt;
     }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
     gpu_module_func.destroy_handle(&ctx);
+    for (uint32_t k = 0; k < g_fake.n; k++) frame_bytes += g_fake.desc[k].len;
 
     out = fopen(argv[3], "wb");
     if (!out || fwrite(status, 1, g_fake.n, out) != g_fake.n) { perror(argv[3]); return 1; }
     fclose(out);
+    secs = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     printf("{\"frames\": %u, \"seen\": %u, \"rounds\": %d, \"inner_bursts\": %d, "
            "\"rx_packets\": %llu, \"rx_errors\": %llu, \"changed\": %llu, "
-           "\"ioctl_rx_ip\": %d, \"ioctl_rx_tcp\": %d}\n",
+           "\"ioctl_rx_ip\": %d, \"ioctl_rx_tcp\": %d, \"seconds\": %.6f, "
+           "\"frame_bytes\": %llu}\n",
            g_fake.n, seen, rounds, g_fake.recv_calls, (unsigned long long)rx_packets,
-           (unsigned long long)rx_errors, (unsigned long long)changed, ioctl_ip, ioctl_tcp);
+           (unsigned long long)rx_errors, (unsigned long long)changed, ioctl_ip, ioctl_tcp, secs,
+           (unsigned long long)frame_bytes);
     return 0;
 }

@@ -448,6 +448,10 @@ int main(int argc, char **argv) {
         vs.push_back({"abl2_rss_sorted_cu2", rx_kernel<kRxChunk, true, 2, 8, true, 6, false, false, 4>, 2});
         vs.push_back({"abl1_rss_sorted_nostore_cu2", rx_kernel<kRxChunk, true, 1, 8, true, 6, false, false, 4, 0>, 2});
         vs.push_back({"norss_sorted_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 4>, 2});
+        vs.push_back({"rss_sorted5t_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 5>, 2});
+        vs.push_back({"rss_sorted6t_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 6>, 2});
+        vs.push_back({"rss_sorted6t_noalign_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 6, 8, false>, 2});
+        vs.push_back({"norss_sorted5t_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 5>, 2});
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     } else {
         vs.push_back({"U6_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false>, 2});
@@ -457,6 +461,9 @@ int main(int argc, char **argv) {
         vs.push_back({"pair_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 2>, 2});
         vs.push_back({"unr1buf_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 3>, 2});
         vs.push_back({"sorted_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 4>, 2});
+        vs.push_back({"sorted5t_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 5>, 2});
+        vs.push_back({"unr1buf_noalign_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 3, 8, false>, 2});
+        vs.push_back({"U6_noalign_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 0, 8, false>, 2});
         if (strcmp(cfg, "c2") == 0) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
             vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
