@@ -110,8 +110,10 @@ def cpu_baseline(host_buf, desc, cfg, sample_n):
     }
 
 
-def pcie_inclusive(ctx, host_buf, desc, nbytes):
-    """Host frames -> H2D -> kernel -> D2H of results, pipelined on 3 streams."""
+def pcie_inclusive(ctx, host_buf, desc, nbytes, world):
+    """Host frames -> H2D -> kernel -> D2H of results, pipelined on 3 streams.
+    Every rank runs its own shard at the same time (each GPU has its own PCIe
+    link); a rep's time is the max over ranks, the best rep is reported."""
     from mtcp_amd import gpu
     gpu.host_register(host_buf)
     try:
@@ -121,18 +123,30 @@ def pcie_inclusive(ctx, host_buf, desc, nbytes):
             ctx.rx_chunk(host_buf, desc, 6, out)   # warm-up (allocates stages)
             best = None
             for _ in range(3):
+                if world > 1:
+                    dist.barrier()
                 t0 = time.perf_counter()
                 ctx.rx_chunk(host_buf, desc, 6, out)
                 dt = time.perf_counter() - t0
+                if world > 1:
+                    t = torch.tensor([dt], dtype=torch.float64)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                    dt = float(t[0])
                 best = dt if best is None else min(best, dt)
         finally:
             gpu.host_unregister(out)
     finally:
         gpu.host_unregister(host_buf)
-    return {"value": round(nbytes / best / 1e9, 3), "unit": "GB/s",
-            "gpkt_per_s": round(len(desc) / best / 1e9, 5),
+    total_bytes, total_pkts = nbytes, len(desc)
+    if world > 1:
+        tb = torch.tensor([nbytes, len(desc)], dtype=torch.int64)
+        dist.all_reduce(tb)
+        total_bytes, total_pkts = int(tb[0]), int(tb[1])
+    return {"value": round(total_bytes / best / 1e9, 3), "unit": "GB/s",
+            "gpkt_per_s": round(total_pkts / best / 1e9, 5), "n_gpus": world,
             "note": "pinned host chunk in, host results out; H2D + kernel + D2H overlapped "
-                    "on 3 streams, 64 MiB stages; wall clock, best of 3"}
+                    "on 3 streams, 64 MiB stages; all ranks at once, wall clock max over "
+                    "ranks, best of 3"}
 
 
 def main():
@@ -208,18 +222,18 @@ def main():
     gpps = total_pkts * args.steps / elapsed / 1e9
 
     extra = {}
-    if rank == 0 and world == 1:
-        want_cpu = args.cpu_baseline == "on" or args.cpu_baseline == "auto"
-        want_pcie = args.pcie == "on" or args.pcie == "auto"
-        if want_cpu or want_pcie:
-            host = d_buf.cpu().numpy()
-            if want_cpu:
-                try:
-                    extra["cpu_baseline"] = cpu_baseline(host, sh.desc, cfg, args.cpu_sample)
-                except Exception as exc:   # report, never fake
-                    extra["cpu_baseline"] = {"value": None, "error": repr(exc)}
-            if want_pcie:
-                extra["pcie_inclusive"] = pcie_inclusive(ctx, host, sh.desc, frame_bytes)
+    want_cpu = rank == 0 and world == 1 and args.cpu_baseline in ("on", "auto")
+    want_pcie = args.pcie in ("on", "auto")     # every rank: a collective step when N > 1
+    if want_cpu or want_pcie:
+        host = d_buf.cpu().numpy()
+        if want_cpu:
+            try:
+                extra["cpu_baseline"] = cpu_baseline(host, sh.desc, cfg, args.cpu_sample)
+            except Exception as exc:   # report, never fake
+                extra["cpu_baseline"] = {"value": None, "error": repr(exc)}
+        if want_pcie:
+            extra["pcie_inclusive"] = pcie_inclusive(ctx, host, sh.desc, frame_bytes, world)
+        del host
     ctx.close()
 
     if rank == 0:

@@ -96,13 +96,13 @@ uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
 
 // Phase-1 schedule by the chunk's average slot size: with mostly large
 // frames (C2 1500 B, C5 9000 B) the 16 rounds unrolled and single-buffered
-// (UNR 3) stream best; with many small frames (C3: half 64 B) the size-sorted
+// (SCHED 3) stream best; with many small frames (C3: half 64 B) the size-sorted
 // rounds win — large frames four per round, double-buffered, small ones
 // sixteen per round (tools/rx_variants, in-process A/B, four boxes: C2
 // unrolled 240.9-243.1 / rolled 244.2-246.0 / sorted 248-250 us; C5 unrolled
 // and rolled equal, 683-686 us; C3 rolled 164, unrolled 145, sorted 141 us).
 // The sorted schedule issues the first two small rounds together with the
-// pre-issued first large round, through L2 (UNR 6): a 64 B frame shares its
+// pre-issued first large round, through L2 (SCHED 6): a 64 B frame shares its
 // 128 B line with a neighbour's edge that another round streams, and the
 // early temporal load lets that round hit it (C3 140.7 -> 134.3 us).
 // Pointer bursts have no chunk size: unrolled.
@@ -114,10 +114,9 @@ uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
 constexpr uint64_t kUnrollBelowSlotBytes = 1024;
 constexpr uint64_t kLineAlignAboveSlotBytes = 1536;
 
-template <int MODE, bool RSS, int UNR, bool LALIGN>
+template <int MODE, bool RSS, int SCHED, bool LALIGN>
 void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
-    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, 0, 8, true, 6, false, false, UNR, 8, LALIGN>), grid,
-                       block, 0, st, kp);
+    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, SCHED, LALIGN>), grid, block, 0, st, kp);
 }
 
 template <int MODE, bool RSS>

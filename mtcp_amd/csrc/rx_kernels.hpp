@@ -184,11 +184,18 @@ struct Trip {
 // every pass.  Stores interleaved with the frame stream cost far more HBM
 // time than their bytes (tools/rx_variants ladder: 40 B/packet written per
 // pass +45 us on C2, written at the end +18 us); DEFER 0 stores per pass.
-// UNR: 0 = rolled trip loop (row broadcasts through a switch); 1 = the 16
-// rounds fully unrolled (constant DPP broadcasts); 2 = a loop over pairs of
-// rounds whose trip info comes from ds_bpermute one round ahead.
-template <int MODE, bool RSS, int ABL = 0, int B = 8, bool NT = true, int U = 6, bool PIPE = false,
-          bool PAIR = false, int UNR = 0, int DEFER = 8, bool LALIGN = true>
+// SCHED, the phase-1 schedule: 0 = rolled trip loop (row broadcasts through
+// a switch); 3 = the 16 rounds unrolled, single-buffered (constant DPP
+// broadcasts); 4 = size-sorted rounds; 5 = sorted, the first two small rounds
+// issued with the first large round through L2; 6 = as 5, issued with the
+// pre-issued first large round at the end of the previous pass.  Dispatched:
+// 3 (large frames) and 6 (small-slot chunks); the others are A/B baselines
+// for tools/rx_variants.hip (earlier variants — double-buffered unrolled
+// rounds, round pairs, software-pipelined trips, per-pass stores interleaved
+// with the next pass's loads — lost on every config and were removed).
+// LALIGN: multi-trip frames stream from the start of their first 128 B line.
+template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
+          bool NT = true, int U = 6>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ WaveLds lds[kWavesPerBlock];
@@ -330,7 +337,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         }
     };
 
-    // ---- size-sorted schedule (UNR == 4) ---------------------------------
+    // ---- size-sorted schedule (SCHED == 4) ---------------------------------
     constexpr uint32_t kSmallChunks = 4;        // <= 64 B on the 16 B grid
     constexpr uint32_t kQuads = kWave / 4;      // small frames per round
     uint32_t pre_nL = 0, pre_nS = 0;            // class counts of the pre-issued pass
@@ -379,9 +386,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     auto small_load = [&](const Trip &t) -> v4u {
         const uint32_t q = lane & 3;
         const uint32_t cc = q < t.nj ? q : (t.nj ? t.nj - 1 : 0u);
-        // UNR 5: small frames load through L2 normally (their 128 B line is
+        // SCHED 5: small frames load through L2 normally (their 128 B line is
         // shared with a neighbour's edge, streamed in another round)
-        return NT && UNR < 5 ? gload_nt(t.base + 16ull * cc) : gload(t.base + 16ull * cc);
+        return NT && SCHED < 5 ? gload_nt(t.base + 16ull * cc) : gload(t.base + 16ull * cc);
     };
     auto small_finish = [&](const Trip &t, const v4u &v) {
         const uint32_t q = lane & 3;
@@ -457,9 +464,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     v4u X[U], Y[U];
     Trip pre;                    // next pass's first trip, already issued into X
     bool have_pre = false;
-    Trip sa, sb;                 // UNR >= 5: the first two small rounds
+    Trip sa, sb;                 // SCHED >= 5: the first two small rounds
     v4u va, vb;
-    bool have_pre_small = false; // UNR 6: already issued into va, vb
+    bool have_pre_small = false; // SCHED 6: already issued into va, vb
     for (uint32_t g0 = 0; g0 < kp.n; g0 += pass_pkts) {
         const Frame f = decode(g0);
         if (!__ballot(f.live)) break;
@@ -471,7 +478,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         const bool has_next = g0 + pass_pkts < kp.n;
 
         // ---------------- phase 1: four frames per wave-instruction ---------
-        if constexpr (UNR >= 4) {
+        if constexpr (SCHED >= 4) {
             // Size-sorted rounds.  The wave's frames are ranked by class:
             // large (> kSmallChunks chunks) frames stream four per round as
             // above (a 16-lane row each, U loads per lane), small ones
@@ -499,11 +506,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                 if (rlane == kRow - 1) wl.sum[t.col] = acc;
                 acc = 0;
             };
-            // UNR 5: the first two small rounds go out with the first large
-            // round, before the large frames around them stream.  UNR 6:
+            // SCHED 5: the first two small rounds go out with the first large
+            // round, before the large frames around them stream.  SCHED 6:
             // they go out even earlier, with the pre-issued first large round
             // at the end of the previous pass (below).
-            if constexpr (UNR >= 5) {
+            if constexpr (SCHED >= 5) {
                 if (have_pre_small) {
                     // issued at the end of the previous pass
                 } else if (RL > 0 && !have_pre) {
@@ -545,7 +552,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
             }
             have_pre = false;
             uint32_t s0 = 0;
-            if constexpr (UNR >= 5) {
+            if constexpr (SCHED >= 5) {
                 if (RS > 0) {
                     small_finish(sa, va);
                     small_finish(sb, vb);
@@ -564,7 +571,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
             if (has_next) {                           // the next pass's first large round
                 const Frame fn = decode(g0 + pass_pkts);
                 prepare(fn, pre_nL, pre_nS);
-                if constexpr (UNR == 6) {
+                if constexpr (SCHED == 6) {
                     small_trip(pre_nS, 0, sa);
                     small_trip(pre_nS, 1, sb);
                     va = small_load(sa);
@@ -577,67 +584,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                     have_pre = true;
                 }
             }
-        } else if constexpr (UNR == 2) {
-            // Rounds in pairs: round i (even) streams in X, i+1 in Y.  The
-            // trip of round i+1 is issued before round i is consumed, and the
-            // trip info of round i+2 (frame 4(i+2)+row's base and chunk count,
-            // fetched from its owner lane with ds_bpermute) is requested
-            // before that, so its LDS latency hides under the stream.
-            auto trip_of = [&](const Frame &fr, int ii, Trip &t) {
-                const int src = 4 * ii + (int)row;                 // the frame's owner lane
-                t.i = ii;
-                t.c0 = 0;
-                t.skip = 0;
-                t.col = (uint32_t)src;
-                t.nj = shfl32(fr.nch, src);
-                t.base = ((uint64_t)shfl32((uint32_t)(fr.p16 >> 32), src) << 32) |
-                         shfl32((uint32_t)fr.p16, src);
-            };
-            Trip cur, nxt;
-            if (!have_pre) {
-                trip_of(f, 0, cur);
-                issue(cur, X);
-            } else {
-                cur = pre;
-            }
-            have_pre = false;
-            trip_of(f, 1, nxt);
-            uint32_t acc = 0;
-            auto finish_round = [&](Trip &t, const v4u (&cb)[U]) {
-                consume(t, cb, acc);
-                while (__ballot(t.c0 + U * kRow < t.nj)) {
-                    t.c0 += U * kRow;
-                    v4u Z[U];
-                    issue(t, Z);
-                    consume(t, Z, acc);
-                }
-                acc = row_sum(acc);
-                if (rlane == kRow - 1) wl.sum[4 * t.i + (int)row] = acc;
-                acc = 0;
-            };
-            for (int i = 0; i < kWave / 4; i += 2) {
-                // round i (X); round i+1 goes out into Y
-                issue(nxt, Y);
-                Trip n2;
-                if (i + 2 < kWave / 4) trip_of(f, i + 2, n2);
-                finish_round(cur, X);
-                cur = nxt;
-                // round i+1 (Y); round i+2 (or the next pass's round 0) into X
-                if (i + 2 < kWave / 4) {
-                    issue(n2, X);
-                    nxt = n2;
-                    trip_of(f, i + 3, n2);
-                } else if (has_next) {
-                    const Frame fn = decode(g0 + pass_pkts);
-                    trip_of(fn, 0, pre);
-                    issue(pre, X);
-                    have_pre = true;
-                }
-                finish_round(cur, Y);
-                cur = nxt;
-                nxt = n2;
-            }
-        } else if constexpr (UNR == 3) {
+        } else if constexpr (SCHED == 3) {
             // The 16 rounds unrolled (constant DPP broadcasts) but single-
             // buffered: each round's loads are issued, then consumed, like
             // the read-only walk of tools/rx_variants (lad_B8_desc); only the
@@ -666,56 +613,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                 issue(n, X);
                 have_pre = true;
             }
-        } else if constexpr (UNR == 1) {
-            // The 16 rounds are unrolled, so every row broadcast is a single
-            // constant DPP move.  Round i's first trip streams in buffer X
-            // (i even) or Y (i odd); it was issued one round earlier (round
-            // 0's at the end of the previous pass), and round i issues round
-            // i+1's before consuming its own, so two trips are in flight.
-            // Further trips of a round (frames > 1536 B) load and consume in
-            // place, alongside the next round's first trip.
-            if (!have_pre) {
-                Trip t;
-                enter_round(f, t, 0);
-                issue(t, X);
-            }
-            have_pre = false;
-            uint32_t acc = 0;
-            static_for<0, kWave / 4>([&](auto I) {
-                constexpr int i = decltype(I)::value;
-                v4u(&cb)[U] = (i & 1) ? Y : X;
-                v4u(&nb)[U] = (i & 1) ? X : Y;
-                Trip t;
-                enter_round(f, t, i);
-                if constexpr (i + 1 < kWave / 4) {
-                    Trip n;
-                    enter_round(f, n, i + 1);
-                    issue(n, nb);
-                } else if (has_next) {
-                    const Frame fn = decode(g0 + pass_pkts);
-                    Trip n;
-                    enter_round(fn, n, 0);
-                    issue(n, nb);
-                    have_pre = true;
-                }
-                consume(t, cb, acc);
-                while (__ballot(t.c0 + U * kRow < t.nj)) {
-                    t.c0 += U * kRow;
-                    v4u Z[U];
-                    issue(t, Z);
-                    consume(t, Z, acc);
-                }
-                acc = row_sum(acc);
-                if (rlane == kRow - 1) wl.sum[4 * i + (int)row] = acc;
-                acc = 0;
-            });
-        } else
-        // Software pipeline: the loads of trip t+1 (or, at the end of the
-        // pass, of the next pass's first trip) are issued before trip t is
-        // consumed; X and Y alternate.  Every step issues exactly U
-        // loads (a finished pipeline loads a harmless dummy) so that the
-        // compiler's counted vmcnt waits stay exact.
-        {
+        } else {
+            // SCHED 0, rolled: one trip at a time through the pass's rounds;
+            // only the next pass's first trip is issued early (before this
+            // pass's phase 2).
             Trip cur;
             bool have;
             if (have_pre) {
@@ -725,92 +626,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                 have = first_trip(f, cur);
                 issue(cur, X);
             }
+            have_pre = false;
             uint32_t acc = 0;
-            // the trip to issue after `c`: within the pass, or the next pass's first
-            auto next_of = [&](const Trip &c, Trip &n, bool &more, bool &pre_ok) {
-                n = c;
-                more = advance(f, n);
-                pre_ok = false;
-                if (!more && has_next) {
-                    const Frame fn = decode(g0 + pass_pkts);
-                    if (__ballot(fn.live) && first_trip(fn, n)) pre_ok = true;
-                }
-                if (!more && !pre_ok) n.nj = 0;                     // dummy (valid base)
-            };
-            auto round_end = [&](const Trip &c, const Trip &n, bool more) {
-                if (!more || n.i != c.i) {                          // frame sums -> LDS
+            while (have) {
+                Trip n = cur;
+                const bool more = advance(f, n);
+                consume(cur, X, acc);
+                if (!more || n.i != cur.i) {                        // frame sums -> LDS
                     acc = row_sum(acc);
-                    if (rlane == kRow - 1) wl.sum[4 * c.i + (int)row] = acc;
+                    if (rlane == kRow - 1) wl.sum[4 * cur.i + (int)row] = acc;
                     acc = 0;
                 }
-            };
-            have_pre = false;
-            if constexpr (!PIPE) {
-                // one trip (PAIR: two trips) at a time; only the next pass's
-                // first trip is issued early (before this pass's phase 2)
-                while (have) {
-                    Trip n = cur;
-                    bool more = advance(f, n);
-                    if constexpr (PAIR) {
-                        if (!more) n.nj = 0;                        // dummy: keeps vmcnt exact
-                        issue(n, Y);                                // both trips in flight
-                    }
-                    consume(cur, X, acc);
-                    round_end(cur, n, more);
-                    if (!more) break;
-                    if constexpr (PAIR) {
-                        cur = n;
-                        consume(cur, Y, acc);
-                        n = cur;
-                        more = advance(f, n);
-                        round_end(cur, n, more);
-                        if (!more) break;
-                    }
-                    issue(n, X);
-                    cur = n;
-                }
-                if (has_next) {
-                    Trip n;
-                    const Frame fn = decode(g0 + pass_pkts);
-                    if (__ballot(fn.live) && first_trip(fn, n)) {
-                        issue(n, X);
-                        pre = n;
-                        have_pre = true;
-                    }
-                }
-                have = false;
-            }
-            while (have) {
-                Trip n;
-                bool more, pre_ok;
-                next_of(cur, n, more, pre_ok);
-                issue(n, Y);
-                consume(cur, X, acc);
-                round_end(cur, n, more);
-                if (!more) {
-                    if (pre_ok) {
-#pragma unroll
-                        for (int u = 0; u < U; ++u) X[u] = Y[u];
-                        pre = n;
-                        have_pre = true;
-                    }
-                    break;
-                }
-                cur = n;
-                next_of(cur, n, more, pre_ok);
+                if (!more) break;
                 issue(n, X);
-                consume(cur, Y, acc);
-                round_end(cur, n, more);
-                if (!more) {
-                    if (pre_ok) {
-                        pre = n;
-                        have_pre = true;
-                    }
-                    break;
-                }
                 cur = n;
             }
-            if (PIPE && !have && has_next) {  // nothing in this pass: start the next one
+            if (has_next) {
                 Trip n;
                 const Frame fn = decode(g0 + pass_pkts);
                 if (__ballot(fn.live) && first_trip(fn, n)) {

@@ -296,84 +296,6 @@ __global__ __launch_bounds__(256) void ladder(mg::KParams kp) {
 }
 
 
-// Writer-wave split: waves 0-3 of a 320-thread workgroup stream frames (as
-// lad_B8_desc) and leave one 40 B record per packet in LDS; wave 4 stores
-// the previous pass's records while the readers stream the next one, so no
-// reader ever waits behind a store.  One LDS-only barrier per pass.
-__global__ __launch_bounds__(320) void ww_ladder(mg::KParams kp) {
-    using namespace mg;
-    __shared__ uint32_t rec[2][4][640];
-    const uint32_t lane = threadIdx.x & 63, row = lane >> 4, rl = lane & 15;
-    const uint32_t wib = threadIdx.x >> 6;
-    const bool writer = wib == 4;
-    const uint32_t nw = gridDim.x * 4;
-    const uint32_t wave = blockIdx.x * 4 + (writer ? 0 : wib);
-    const uint64_t base = (uint64_t)(uintptr_t)kp.buf;
-    auto map = [&](uint32_t l) -> uint32_t { return (l / 8) * (nw * 8) + wave * 8 + (l % 8); };
-    const uint32_t pass_pkts = nw * 64;
-    const uint32_t npass = (kp.n + pass_pkts - 1) / pass_pkts;
-    for (uint32_t ps = 0; ps <= npass; ++ps) {
-        const uint32_t g0 = ps * pass_pkts;
-        if (!writer && ps < npass) {
-            uint32_t r_lo = 0, r_hi = 0, r_n = 0;
-            const uint32_t k = g0 + map(lane);
-            {
-                uint64_t p = base;
-                uint32_t nch = 0;
-                if (k < kp.n) {
-                    const uint64_t raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
-                    p = base + ((uint64_t)(uint32_t)raw << kp.off_shift);
-                    const uint32_t L = (uint32_t)(raw >> 32) & 0xFFFFu;
-                    nch = (uint32_t)((((p + L + 15) & ~15ull) - (p & ~15ull)) >> 4);
-                }
-                const int src = 4 * (int)rl + (int)row;
-                r_n = shfl32(nch, src);
-                r_lo = shfl32((uint32_t)p, src);
-                r_hi = shfl32((uint32_t)(p >> 32), src);
-            }
-            uint32_t acc = 0;
-            static_for<0, 16>([&](auto I) {
-                constexpr int i = decltype(I)::value;
-                const uint32_t nj = row_bcast(r_n, i);
-                const uint64_t fb = ((uint64_t)row_bcast(r_hi, i) << 32) | row_bcast(r_lo, i);
-                v4u x[6];
-#pragma unroll
-                for (int u = 0; u < 6; ++u) {
-                    const uint32_t c = u * 16 + rl;
-                    const uint32_t cc = c < nj ? c : (nj ? nj - 1 : 0u);
-                    x[u] = gload_nt(fb + 16ull * cc);
-                }
-#pragma unroll
-                for (int u = 0; u < 6; ++u) {
-                    const uint32_t s4 = halves4(x[u], 0u);
-                    acc += (u * 16 + rl < nj) ? s4 : 0u;
-                }
-            });
-            uint32_t *r = &rec[ps & 1][wib][lane * 10];
-#pragma unroll
-            for (int q = 0; q < 10; ++q) r[q] = acc + q;
-        }
-        if (writer && ps > 0) {
-            // pass ps-1: reader wave w's lanes l own packets map_w(l); runs of 8
-            const uint32_t gp = (ps - 1) * pass_pkts;
-            for (uint32_t w = 0; w < 4; ++w) {
-                const uint32_t *r = rec[(ps - 1) & 1][w];
-                const uint32_t ww_wave = blockIdx.x * 4 + w;
-                for (uint32_t q = lane; q < 320; q += 64) {
-                    const uint32_t run = q / 40, d = q % 40;
-                    const uint32_t pk = gp + run * (nw * 8) + ww_wave * 8;
-                    const uint64_t val = (uint64_t)r[run * 80 + 2 * d] |
-                                         ((uint64_t)r[run * 80 + 2 * d + 1] << 32);
-                    if (pk < kp.n) reinterpret_cast<uint64_t *>(kp.out + pk)[d] = val;
-                }
-            }
-        }
-        // LDS-only barrier: no vmcnt wait, so neither the readers' prefetch nor
-        // the writer's stores are drained here
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-}
-
 struct Variant { const char *name; kfn fn; uint32_t blocks_per_cu; };
 
 static uint64_t mix(uint64_t z) {
@@ -437,43 +359,38 @@ int main(int argc, char **argv) {
     std::vector<Variant> vs;
     using namespace mg;
     if (rss) {
-        vs.push_back({"rss_U6_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false>, 4});
-        vs.push_back({"rss_U6_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false>, 2});
-        vs.push_back({"rss_defer0_cu4", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 0, 0>, 4});
-        vs.push_back({"rss_unr_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 1>, 2});
-        vs.push_back({"rss_pair_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 2>, 2});
-        vs.push_back({"rss_unr1buf_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 3>, 2});
-        vs.push_back({"rss_sorted_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 4>, 2});
-        vs.push_back({"abl1_rss_sorted_cu2", rx_kernel<kRxChunk, true, 1, 8, true, 6, false, false, 4>, 2});
-        vs.push_back({"abl2_rss_sorted_cu2", rx_kernel<kRxChunk, true, 2, 8, true, 6, false, false, 4>, 2});
-        vs.push_back({"abl1_rss_sorted_nostore_cu2", rx_kernel<kRxChunk, true, 1, 8, true, 6, false, false, 4, 0>, 2});
-        vs.push_back({"norss_sorted_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 4>, 2});
-        vs.push_back({"rss_sorted5t_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 5>, 2});
-        vs.push_back({"rss_sorted6t_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 6>, 2});
-        vs.push_back({"rss_sorted6t_noalign_cu2", rx_kernel<kRxChunk, true, 0, 8, true, 6, false, false, 6, 8, false>, 2});
-        vs.push_back({"norss_sorted5t_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 5>, 2});
+        // variant 0 = what mtcp_gpu.hip dispatches for C3; every other variant's
+        // records must equal its records byte for byte
+        vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
+        vs.push_back({"rss_rolled_cu2", rx_kernel<kRxChunk, true, 0>, 2});
+        vs.push_back({"rss_unrolled_cu2", rx_kernel<kRxChunk, true, 3>, 2});
+        vs.push_back({"rss_sorted_cu2", rx_kernel<kRxChunk, true, 4>, 2});
+        vs.push_back({"rss_sorted5_cu2", rx_kernel<kRxChunk, true, 5>, 2});
+        vs.push_back({"rss_sorted6_cu3", rx_kernel<kRxChunk, true, 6>, 3});
+        vs.push_back({"rss_sorted6_defer0_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 0>, 2});
+        vs.push_back({"abl1_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 1>, 2});
+        vs.push_back({"abl2_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 2>, 2});
+        vs.push_back({"abl1_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0>, 2});
+        vs.push_back({"norss_sorted6_cu2", rx_kernel<kRxChunk, false, 6>, 2});
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     } else {
-        vs.push_back({"U6_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false>, 2});
-        vs.push_back({"defer0_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 0, 0>, 2});
-        vs.push_back({"defer4_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 0, 4>, 2});
-        vs.push_back({"unr_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 1>, 2});
-        vs.push_back({"pair_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 2>, 2});
-        vs.push_back({"unr1buf_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 3>, 2});
-        vs.push_back({"sorted_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 4>, 2});
-        vs.push_back({"sorted5t_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 5>, 2});
-        vs.push_back({"unr1buf_noalign_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 3, 8, false>, 2});
-        vs.push_back({"U6_noalign_cu2", rx_kernel<kRxChunk, false, 0, 8, true, 6, false, false, 0, 8, false>, 2});
+        // variant 0 = what mtcp_gpu.hip dispatches for C2 (C5 adds LALIGN)
+        vs.push_back({"unrolled_cu2", rx_kernel<kRxChunk, false, 3>, 2});
+        vs.push_back({"unrolled_lalign_cu2", rx_kernel<kRxChunk, false, 3, true>, 2});
+        vs.push_back({"rolled_cu2", rx_kernel<kRxChunk, false, 0>, 2});
+        vs.push_back({"rolled_lalign_cu2", rx_kernel<kRxChunk, false, 0, true>, 2});
+        vs.push_back({"unrolled_cu3", rx_kernel<kRxChunk, false, 3>, 3});
+        vs.push_back({"unrolled_defer0_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 0>, 2});
+        vs.push_back({"unrolled_defer4_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 4>, 2});
+        vs.push_back({"sorted_cu2", rx_kernel<kRxChunk, false, 4>, 2});
+        vs.push_back({"sorted6_cu2", rx_kernel<kRxChunk, false, 6>, 2});
+        vs.push_back({"abl1_unrolled_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0>, 2});
         if (strcmp(cfg, "c2") == 0) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
             vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
             vs.push_back({"lad_B8_desc_st3", ladder<8, true, 0, 3, false>, 2});
-            vs.push_back({"lad_B8_desc_st7_atend", ladder<8, true, 0, 7, false>, 2});
             vs.push_back({"lad_B8_desc_st12_regs_atend", ladder<8, true, 0, 12, false>, 2});
-            vs.push_back({"lad_B8_desc_st13_regs_coal8", ladder<8, true, 0, 13, false>, 2});
-            vs.push_back({"lad_B8_desc_st14_regs_nt", ladder<8, true, 0, 14, false>, 2});
             vs.push_back({"lad_B8_desc_st15_regs_coal16", ladder<8, true, 0, 15, false>, 2});
-            vs.push_back({"lad_B8_desc_st8_private", ladder<8, true, 0, 8, false>, 2});
         }
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     }
@@ -490,7 +407,7 @@ int main(int argc, char **argv) {
             if (blocks > cus * vs[v].blocks_per_cu) blocks = cus * vs[v].blocks_per_cu;
             kp.out = v == 0 ? d_ref : d_out;
             CK(hipMemset(kp.out, 0, n * sizeof(mtcp_gpu_result)));
-            const uint32_t threads = strncmp(vs[v].name, "ww_", 3) == 0 ? 320 : 256;
+            const uint32_t threads = 256;
             hipLaunchKernelGGL(vs[v].fn, dim3(blocks), dim3(threads), 0, 0, kp);
             CK(hipEventRecord(a));
             for (int i = 0; i < reps; ++i)
@@ -500,7 +417,7 @@ int main(int argc, char **argv) {
             float t;
             CK(hipEventElapsedTime(&t, a, b));
             ms[v].push_back(t / reps);
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "norss") && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && strncmp(vs[v].name, "ww_", 3) != 0) {
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "norss") && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad")) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
