@@ -1,0 +1,86 @@
+"""Frames at every 4-byte alignment inside a 128 B line, through each phase-1
+schedule the library dispatches (mtcp_gpu.hip launch_sched): size-sorted
+rounds (average slot < 1 KiB), unrolled rounds (<= 1536 B) and unrolled
+rounds with line-aligned trips (> 1536 B, rx_kernel LALIGN, where the first
+trip of a multi-trip frame starts (p16 & 127) / 16 chunks before the frame).
+Multi-trip frames (> 1536 B) appear in all three.  Frames come from the
+oracle's generator (valid checksums, a few corrupted), are moved to the
+offsets under test, and every field of every record must equal the oracle's.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from mtcp_amd import DESC_DTYPE, RESULT_DTYPE, pktgen
+from tests.test_gpu_parity import DEV, assert_same, dev_results, run_rx_dev, to_dev
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    from mtcp_amd import gpu as g
+    return g
+
+
+def _lengths(kind, n, rng):
+    if kind == "jumbo":                      # average slot > 1536 B: LALIGN
+        return rng.integers(1537, 9001, n)
+    if kind == "mid":                        # 1024 .. 1536 B: unrolled, no LALIGN
+        return np.where(rng.random(n) < 0.12, rng.integers(1537, 3000, n), rng.integers(900, 1200, n))
+    return np.where(rng.random(n) < 0.08, rng.integers(1537, 9001, n), 64)   # < 1 KiB: sorted
+
+
+def _unaligned_batch(kind, n=1536, seed=11):
+    """Generator frames re-packed so that frame i starts at 4*(i % 32) mod 128."""
+    rng = np.random.default_rng(seed)
+    lens = _lengths(kind, n, rng).astype(np.uint16)
+    desc64, nbytes = pktgen.layout_from_lengths(lens, 6)
+    src = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(src, desc64, 6, seed, 0)
+    offs = np.zeros(n, np.int64)
+    pos = 0
+    for i in range(n):
+        pos = (pos + 127) & ~127                     # next line, then the alignment under test
+        offs[i] = pos + 4 * (i % 32)
+        pos = offs[i] + int(lens[i])
+    buf = np.zeros(((pos + 127) & ~127) + 128, np.uint8)
+    s0 = desc64["offset"].astype(np.int64) << 6
+    for i in range(n):
+        buf[offs[i]:offs[i] + lens[i]] = src[s0[i]:s0[i] + lens[i]]
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    desc["offset"] = offs.astype(np.uint32)
+    desc["len"] = lens
+    return buf, desc
+
+
+@pytest.mark.parametrize("kind,slot_lo,slot_hi", [("jumbo", 1537, 1 << 30), ("mid", 1024, 1536),
+                                                  ("small", 0, 1023)])
+def test_unaligned_frames_every_schedule(gpu, kind, slot_lo, slot_hi):
+    buf, desc = _unaligned_batch(kind)
+    padded = buf.nbytes + (-buf.nbytes) % 16
+    assert slot_lo <= padded // len(desc) <= slot_hi        # the schedule under test is dispatched
+    assert (desc["len"] > 1536).sum() > 50                    # multi-trip frames present
+    with gpu.Context(0, rss=True, rss_queues=8) as ctx:
+        got = run_rx_dev(ctx, buf, desc, 0)
+    want = oracle.rx_chunk(buf, desc, 0, oracle.rss_cfg(None, 8, 1))
+    assert_same(got, want, kind)
+    assert (got["verdict"] == 0).mean() > 0.95
+
+
+def test_unaligned_frames_pointer_burst(gpu):
+    """The same frames as a (pointer, len) burst: rx_ptrs always streams with
+    line-aligned trips, whatever the frame sizes."""
+    buf, desc = _unaligned_batch("small", seed=12)
+    b = to_dev(buf)
+    ptrs = torch.from_numpy(desc["offset"].astype(np.int64) + b.data_ptr()).to(DEV)
+    lens = torch.from_numpy(desc["len"].astype(np.int16)).to(DEV)
+    out = dev_results(len(desc))
+    with gpu.Context(0) as ctx:
+        ctx.rx_ptrs_dev(ptrs, lens, len(desc), out)
+        torch.cuda.synchronize()
+    got = out.cpu().numpy().view(RESULT_DTYPE)
+    assert_same(got, oracle.rx_chunk(buf, desc, 0), "pointer burst")
