@@ -6,7 +6,7 @@
 # usage: tools/profile_config.sh CONFIG OUTDIR
 cfg=$1; out=$2
 mkdir -p "$out"
-b="python3 bench.py --config $cfg --steps 30 --warmup 3 --cpu-baseline off --pcie off"
+b="python3 bench.py --config $cfg --steps 200 --warmup 20 --cpu-baseline off --pcie off"
 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$out/trace" -o run -- $b > "$out/trace.log" 2>&1 || exit $?
 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$out/fetch" -o run -- $b > "$out/fetch.log" 2>&1 || exit $?
 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d "$out/write" -o run -- $b > "$out/write.log" 2>&1 || exit $?
