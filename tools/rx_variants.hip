@@ -389,6 +389,9 @@ int main(int argc, char **argv) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
             vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
             vs.push_back({"lad_B8_desc_st3", ladder<8, true, 0, 3, false>, 2});
+            vs.push_back({"lad_B8_desc_st4_nt", ladder<8, true, 0, 4, false>, 2});
+            vs.push_back({"lad_B8_desc_st5_sys", ladder<8, true, 0, 5, false>, 2});
+            vs.push_back({"lad_B8_desc_st11_coal16_perpass", ladder<8, true, 0, 11, false>, 2});
             vs.push_back({"lad_B8_desc_st12_regs_atend", ladder<8, true, 0, 12, false>, 2});
             vs.push_back({"lad_B8_desc_st15_regs_coal16", ladder<8, true, 0, 15, false>, 2});
         }
