@@ -48,12 +48,23 @@ CONFIGS = {
 }
 
 
+# SURVEY §8(f) rows beside the rx path, each measured on one GPU (not the
+# headline line): f1 tx checksum fill over the C2 batch, f3 HashFlow over the
+# rx records of the C2 batch, f4 the RSS queue map of CreateAddressPoolPerCore's
+# candidate space (num_addr x 64511 ports).
+ROWS = {
+    "f1": "tx checksum fill (ip_out.c:94,164, tcp_out.c:211,329) over 1 M x 1500 B frames",
+    "f3": "HashFlow (tcp_stream.c:56-90) over 1 M rx records of the C2 batch",
+    "f4": "RSS queue of 64 addresses x 64511 ports (addr_pool.c:155-178, rss.c:90-103)",
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + sorted(ROWS))
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
                     help="packets in the CPU sample (default: the whole 1-GPU batch, "
@@ -149,8 +160,139 @@ def pcie_inclusive(ctx, host_buf, desc, nbytes, world):
                     "ranks, best of 3"}
 
 
+def _timed(step, steps, warmup, stream):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, ev0.elapsed_time(ev1) / steps / 1e3
+
+
+def _cpu_time(fn, reps=3):
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return best
+
+
+def run_row(args):
+    """One §8(f) row on one GPU; prints one JSON line of the headline's shape."""
+    from mtcp_amd import gpu
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1 or args.gpus != 1:
+        raise SystemExit("the f-row benches run on one GPU")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    want_cpu = args.cpu_baseline in ("on", "auto")
+    line = {"metric": f"{args.config}: " + ROWS[args.config], "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "data": "synthetic", "config": {"workload": args.config}}
+    n, seed = 1 << 20, 2
+    if args.config in ("f1", "f3"):
+        desc, nbytes = pktgen.layout(n, 1500, 6, seed)
+        d_buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+        gpu.pktgen_dev(d_buf, d_desc, n, 6, seed, stream=stream)
+        frame_bytes = int(desc["len"].astype(np.int64).sum())
+    ctx = gpu.Context(0)
+    if args.config == "f1":
+        # idempotent after the first fill: every step rewrites the same checks
+        step = lambda: ctx.tx_fill_dev(d_buf, d_desc, n, 6, stream=stream)
+        wall, kern = _timed(step, args.steps, args.warmup, stream)
+        algo = frame_bytes + 4 * n
+        line.update(value=round(frame_bytes / wall / 1e9, 2), unit="GB/s", dtype="u8",
+                    ms_per_step=round(wall * 1e3, 5), gpkt_per_s=round(n / wall / 1e9, 4))
+        line["roofline"] = {"bound": "hbm", "achieved": round(algo / kern / 1e9, 2),
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                            "avg_launch_ms": round(kern * 1e3, 5),
+                            "algorithmic_bytes_per_launch": algo,
+                            "note": "sum L read + 4 B of check fields written per frame"}
+        if want_cpu:
+            import oracle   # test infrastructure: the baseline leg only
+            host = d_buf.cpu().numpy()
+            m = 1 << 18
+            sub = desc[:m]
+            end = (int(sub["offset"][-1]) << 6) + 1536
+            hb = np.ascontiguousarray(host[:end])
+            t = _cpu_time(lambda: oracle.tx_fill(hb, sub, 6))
+            sb = int(sub["len"].astype(np.int64).sum())
+            line["cpu_baseline"] = {"value": round(sb / t / 1e9, 3), "unit": "GB/s", "cores": 1,
+                                    "kind": "port", "sample": f"first {m} frames, best of 3 "
+                                    "(oracle/mtcp_oracle.c tx fill, gcc -O3)"}
+    elif args.config == "f3":
+        d_out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+        ctx.rx_chunk_dev(d_buf, d_desc, n, 6, d_out, stream=stream)
+        bins = torch.empty(n, dtype=torch.int32, device=dev)
+        step = lambda: ctx.flow_hash_dev(d_out, n, bins, stream=stream)
+        wall, kern = _timed(step, args.steps, args.warmup, stream)
+        algo = n * (40 + 4)
+        line.update(value=round(n / wall / 1e9, 4), unit="Gpkt/s", dtype="u32",
+                    ms_per_step=round(wall * 1e3, 5))
+        line["roofline"] = {"bound": "hbm", "achieved": round(algo / kern / 1e9, 2),
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                            "avg_launch_ms": round(kern * 1e3, 5),
+                            "algorithmic_bytes_per_launch": algo,
+                            "note": "40 B record read (its 12 key bytes and verdict span the "
+                                    "record's lines) + 4 B bin written per packet"}
+        if want_cpu:
+            import oracle
+            res = d_out.cpu().numpy().view(gpu.RESULT_DTYPE)
+            t = _cpu_time(lambda: oracle.flow_bins(res))
+            line["cpu_baseline"] = {"value": round(n / t / 1e9, 4), "unit": "Gpkt/s", "cores": 1,
+                                    "kind": "port", "sample": f"the same {n} records, best of 3 "
+                                    "(oracle/mtcp_oracle.c HashFlow, gcc -O3)"}
+    else:
+        num_addr, nq = 64, 16
+        total = num_addr * (gpu.MAX_PORT - gpu.MIN_PORT)
+        queue = torch.empty(total, dtype=torch.uint8, device=dev)
+        base_h, daddr_h, dport_h = 0x0A000001, 0xC0A80001, 80
+        step = lambda: ctx.rss_queue_map_dev(base_h, num_addr, daddr_h, dport_h, nq, True, queue,
+                                             stream=stream)
+        wall, kern = _timed(step, args.steps, args.warmup, stream)
+        line.update(value=round(total / wall / 1e9, 3), unit="Gcandidates/s", dtype="u32",
+                    ms_per_step=round(wall * 1e3, 5))
+        line["roofline"] = {"bound": "lds", "achieved": None, "peak": None, "unit": None,
+                            "frac": None, "traffic": None, "avg_launch_ms": round(kern * 1e3, 5),
+                            "note": "24 LDS nibble-table reads per candidate (Toeplitz over 96 "
+                                    "bits) and 1 B written: bound by LDS lookups, not HBM "
+                                    f"({total} B written per launch)"}
+        import socket
+        import struct
+        b_n = struct.unpack("<I", socket.inet_aton("10.0.0.1"))[0]
+        d_n = struct.unpack("<I", socket.inet_aton("192.168.0.1"))[0]
+        p_n = struct.unpack("<H", struct.pack(">H", 80))[0]
+        t_gpu = _cpu_time(lambda: ctx.addr_pool_search(3, nq, b_n, num_addr, d_n, p_n, True))
+        line["search_end_to_end"] = {"value": round(total / t_gpu / 1e9, 3), "unit": "Gcandidates/s",
+                                     "note": "mtcp_gpu_addr_pool_search host call: queue map, "
+                                             "count / scan / emit compaction, D2H of one core's "
+                                             "entries; wall clock, best of 3"}
+        if want_cpu:
+            import oracle
+            t = _cpu_time(lambda: oracle.addr_pool_search(None, 3, nq, b_n, num_addr, d_n, p_n, 1))
+            line["cpu_baseline"] = {"value": round(total / t / 1e9, 4), "unit": "Gcandidates/s",
+                                    "cores": 1, "kind": "port",
+                                    "sample": "the same search (core 3 of 16 queues, 64 addresses), "
+                                              "best of 3 (oracle/mtcp_oracle.c, gcc -O3)"}
+    ctx.close()
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.config in ROWS:
+        return run_row(args)
     cfg = CONFIGS[args.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -460,6 +460,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         }
     };
 
+    // tx fill: the two check fields of each frame (iph->check at byte 24,
+    // tcph->check at T + 16) are held for up to kTxDefer passes and written
+    // together at the end: sub-dword stores into the frames interleaved with
+    // the read stream cost like the rx records' per-pass stores.
+    constexpr int kTxDefer = MODE == kTxChunk && DEFER > 0 ? DEFER : 0;
+    uint32_t tkeep[kTxDefer > 0 ? kTxDefer : 1][4];
+    uint32_t tx_held = 0;                         // wave-uniform
+    auto tx_write = [&](const uint32_t (&w)[4]) {
+        if (w[3]) {
+            uint16_t *q16 = reinterpret_cast<uint16_t *>(((uint64_t)w[1] << 32) | w[0]);
+            q16[12] = (uint16_t)w[2];                                // iph->check (byte 24)
+            q16[(w[3] + 16) >> 1] = (uint16_t)(w[2] >> 16);          // tcph->check (tcp_out.c:329)
+        }
+    };
+    auto tx_flush = [&]() {
+        if constexpr (kTxDefer > 0) {
+#pragma unroll
+            for (int q = 0; q < kTxDefer; ++q)
+                if ((uint32_t)q < tx_held) tx_write(tkeep[q]);
+            tx_held = 0;
+        }
+    };
+    auto tx_push = [&](const uint32_t (&w)[4]) {
+        if constexpr (kTxDefer > 0) {
+            if (tx_held == (uint32_t)kTxDefer) tx_flush();
+#pragma unroll
+            for (int q = kTxDefer - 1; q > 0; --q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) tkeep[q][i] = tkeep[q - 1][i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tkeep[0][i] = w[i];
+            ++tx_held;
+        }
+    };
+
     fetch(0);
     v4u X[U], Y[U];
     Trip pre;                    // next pass's first trip, already issued into X
@@ -843,12 +878,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         }
 
         if constexpr (MODE == kTxChunk) {
+            uint32_t fill[4] = {0, 0, 0, 0};                        // {p lo, p hi, checks, T}
             if (live && need_sum) {
                 const uint32_t ipc = fold_csum(s_ip - (h[6] & 0xFFFFu));   // ip_out.c:145,164
-                uint16_t *q16 = reinterpret_cast<uint16_t *>(p);
-                q16[12] = (uint16_t)ipc;                              // iph->check (byte 24)
-                q16[(T + 16) >> 1] = (uint16_t)tcp_csum;              // tcph->check (tcp_out.c:329)
+                fill[0] = (uint32_t)p;
+                fill[1] = (uint32_t)(p >> 32);
+                fill[2] = ipc | (tcp_csum << 16);
+                fill[3] = T;
                 if (kp.fill_count) atomicAdd(kp.fill_count, 1u);
+            }
+            if constexpr (kTxDefer > 0) {
+                tx_push(fill);
+            } else {
+                tx_write(fill);
             }
         } else if constexpr (kDefer > 0) {
             const uint32_t r[10] = {saddr, daddr, ports, seq, ack, window | (ip_len << 16),
@@ -877,6 +919,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         }
     }
     flush();
+    tx_flush();
 }
 
 }  // namespace mg

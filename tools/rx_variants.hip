@@ -396,6 +396,9 @@ int main(int argc, char **argv) {
             vs.push_back({"lad_B8_desc_st15_regs_coal16", ladder<8, true, 0, 15, false>, 2});
         }
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
+        // tx fill last: it repairs the corrupted frames the rx variants compare on
+        vs.push_back({"tx_unrolled_cu2", rx_kernel<kTxChunk, false, 3>, 2});
+        vs.push_back({"tx_unrolled_nodefer_cu2", rx_kernel<kTxChunk, false, 3, false, 0, 0>, 2});
     }
     if (single) vs.resize(1);
     hipEvent_t a, b;
@@ -420,7 +423,7 @@ int main(int argc, char **argv) {
             float t;
             CK(hipEventElapsedTime(&t, a, b));
             ms[v].push_back(t / reps);
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "norss") && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad")) {
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad")) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
