@@ -62,6 +62,27 @@ bool hip_ok(hipError_t e, const char *what) {
 }
 #define HIP_OK(x) hip_ok((x), #x)
 
+// Makes `device` current for one ABI call and restores the caller's device
+// on return: an mTCP thread (or a torch process) keeps the device it chose.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false, switched = false;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev == device) {
+            ok = true;
+        } else {
+            ok = HIP_OK(hipSetDevice(device));
+            switched = ok && prev >= 0;
+        }
+    }
+    ~DeviceGuard() {
+        if (switched) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 // util/rss.c:13-105 (BuildKeyCache), then the 24 nibble tables the kernel
 // XORs: table[t][v] = XOR of cache[4t + m] over the bits of nibble v, MSB
 // first (nibble t of the 96-bit input sip|dip|sp|dp, most significant first).
@@ -220,7 +241,8 @@ int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rs
     if ((flags & MTCP_GPU_F_RSS) && rss_num_queues < 1) return MTCP_GPU_EINVAL;
     int ndev = 0;
     if (!HIP_OK(hipGetDeviceCount(&ndev)) || device < 0 || device >= ndev) return MTCP_GPU_ENODEV;
-    if (!HIP_OK(hipSetDevice(device))) return MTCP_GPU_ENODEV;
+    DeviceGuard dg(device);
+    if (!dg.ok) return MTCP_GPU_ENODEV;
 
     mtcp_gpu_ctx *ctx = new (std::nothrow) mtcp_gpu_ctx();
     if (!ctx) return MTCP_GPU_ENOMEM;
@@ -253,7 +275,7 @@ int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rs
 
 void mtcp_gpu_close(mtcp_gpu_ctx *ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto &s : ctx->stage) {
         if (s.stream) {
@@ -291,7 +313,7 @@ void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nu
 
 int mtcp_gpu_sync(mtcp_gpu_ctx *ctx) {
     if (!ctx) return MTCP_GPU_EINVAL;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     return HIP_OK(hipStreamSynchronize(ctx->stream)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
 
@@ -301,7 +323,7 @@ int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len
     if (!ctx || (n && (!d_buf || !d_desc || !d_out)) || off_shift > 16 || (buf_len & 15) ||
         ((uintptr_t)d_buf & 15) || ((uintptr_t)d_out & 7) || ((uintptr_t)d_desc & 7))
         return MTCP_GPU_EINVAL;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     mg::KParams kp = base_params(ctx);
     kp.buf = static_cast<const uint8_t *>(d_buf);
     kp.buf_len = buf_len;
@@ -316,7 +338,7 @@ int mtcp_gpu_rx_ptrs_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts, const 
                          uint32_t n, mtcp_gpu_result *d_out, void *stream) {
     if (!ctx || (n && (!d_pkts || !d_lens || !d_out)) || ((uintptr_t)d_out & 7))
         return MTCP_GPU_EINVAL;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     mg::KParams kp = base_params(ctx);
     kp.ptrs = d_pkts;
     kp.lens = d_lens;
@@ -331,7 +353,7 @@ int mtcp_gpu_tx_fill_dev(mtcp_gpu_ctx *ctx, void *d_buf, uint64_t buf_len,
     if (!ctx || (n && (!d_buf || !d_desc)) || off_shift > 16 || (buf_len & 15) ||
         ((uintptr_t)d_buf & 15) || ((uintptr_t)d_desc & 7))
         return MTCP_GPU_EINVAL;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     mg::KParams kp = base_params(ctx);
     kp.buf = static_cast<const uint8_t *>(d_buf);
     kp.buf_len = buf_len;
@@ -350,7 +372,7 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
                       mtcp_gpu_result *out) {
     if (!ctx || (n && (!buf || !desc || !out)) || off_shift > 16) return MTCP_GPU_EINVAL;
     if (n == 0) return MTCP_GPU_OK;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     int rc = MTCP_GPU_OK;
     if (!offsets_sorted(desc, n)) {
         // arbitrary order: stage the whole chunk once, then batches of descriptors
@@ -427,7 +449,7 @@ int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16
                      uint32_t n, mtcp_gpu_result *out) {
     if (!ctx || (n && (!pkts || !lens || !out))) return MTCP_GPU_EINVAL;
     if (n == 0) return MTCP_GPU_OK;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     // gather into a pinned PSIO-style chunk (64 B aligned slots, pslib.c:146)
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) total += ((uint64_t)lens[i] + 63) & ~63ull;
@@ -465,7 +487,7 @@ int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mt
     if (!ctx || (n && (!buf || !desc)) || off_shift > 16) return MTCP_GPU_EINVAL;
     if (n_filled) *n_filled = 0;
     if (n == 0) return MTCP_GPU_OK;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     Stage &s = ctx->stage[0];
     const uint64_t cap = (buf_len + 15) & ~15ull;
     int rc = stage_reserve(s, cap + 16, n);
@@ -500,7 +522,7 @@ int mtcp_gpu_flow_hash_dev(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *d_res, uint
     if (!ctx || (n && (!d_res || !d_bins)) || ((uintptr_t)d_res & 7) || ((uintptr_t)d_bins & 3))
         return MTCP_GPU_EINVAL;
     if (n == 0) return MTCP_GPU_OK;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     const uint32_t blocks = std::min<uint32_t>((n + mg::kBlock - 1) / mg::kBlock,
                                                (uint32_t)ctx->num_cu * 8);
     hipLaunchKernelGGL(mg::flow_hash_kernel, dim3(blocks), dim3(mg::kBlock), 0, pick(ctx, stream),
@@ -512,7 +534,7 @@ int mtcp_gpu_flow_hash(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *res, uint32_t n
                        uint32_t *bins) {
     if (!ctx || (n && (!res || !bins))) return MTCP_GPU_EINVAL;
     if (n == 0) return MTCP_GPU_OK;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     Stage &s = ctx->stage[0];
     int rc = stage_reserve(s, (uint64_t)n * sizeof(uint32_t), n);
     if (rc != MTCP_GPU_OK) return rc;
@@ -535,7 +557,7 @@ int mtcp_gpu_rss_queue_map_dev(mtcp_gpu_ctx *ctx, uint32_t saddr_base_h, uint32_
     if (!ctx || num_queues < 1 || (num_addr && !d_queue) || ((uintptr_t)d_queue & 3))
         return MTCP_GPU_EINVAL;
     if (num_addr == 0) return MTCP_GPU_OK;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     mg::PoolParams pp{};
     pp.rss_tables = ctx->d_rss_tables;
     pp.saddr_base_h = saddr_base_h;
@@ -563,7 +585,7 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues, uint3
     if (total > (uint64_t)INT32_MAX) return MTCP_GPU_EINVAL;
     const uint32_t num_entry = (uint32_t)((int)total / num_queues);
     if (num_addr == 0 || core < 0 || core >= num_queues) return MTCP_GPU_OK;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dg(ctx->device);
     const uint32_t nb = (uint32_t)((total + mg::kPoolTile - 1) / mg::kPoolTile);
     const uint32_t limit = std::min(num_entry, max_out);
     const uint64_t qbytes = (total + 15) & ~15ull;
