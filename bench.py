@@ -37,6 +37,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 
 # BASELINE.json configs; per_gpu = packets per rank (weak scaling)
 CONFIGS = {
+    # C1 is the reference's CPU-runnable case; on the GPU it is launch-bound
+    # (64 K x 64 B = 4 MB per launch), reported for completeness beside the
+    # reference's code on the same frames
+    "c1": dict(size=64, per_gpu=1 << 16, rss=False, seed=1,
+               desc="64 K x 64 B TCP segments, checksum + parse"),
     "c2": dict(size=1500, per_gpu=1 << 20, rss=False, seed=2,
                desc="1 M x 1500 B (MTU) packets, IP+TCP checksum + header parse"),
     "c3": dict(size="bimodal", per_gpu=1 << 20, rss=True, seed=3,

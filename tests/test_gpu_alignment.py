@@ -84,3 +84,39 @@ def test_unaligned_frames_pointer_burst(gpu):
         torch.cuda.synchronize()
     got = out.cpu().numpy().view(RESULT_DTYPE)
     assert_same(got, oracle.rx_chunk(buf, desc, 0), "pointer burst")
+
+
+def test_maximum_length_frames(gpu):
+    """Frames up to the u16 maximum (65 535 B: 43 trips, tot_len 65 521, a TCP
+    sum of 32 760 words — still exact in 32 bits), at odd 4-byte alignments,
+    with and without a flipped payload bit; chunk mode and pointer burst."""
+    lens = np.array([65535, 65534, 65533, 40001, 16385, 9001, 1537, 65535] * 4, dtype=np.uint16)
+    n = len(lens)
+    desc64, nbytes = pktgen.layout_from_lengths(lens, 6)
+    src = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(src, desc64, 6, 21, 0)
+    offs, pos = np.zeros(n, np.int64), 0
+    for i in range(n):
+        pos = ((pos + 127) & ~127) + 4 * (7 * i % 32)
+        offs[i] = pos
+        pos += int(lens[i])
+    buf = np.zeros(((pos + 127) & ~127) + 128, np.uint8)
+    s0 = desc64["offset"].astype(np.int64) << 6
+    for i in range(n):
+        buf[offs[i]:offs[i] + lens[i]] = src[s0[i]:s0[i] + lens[i]]
+    for i in range(1, n, 3):                               # a payload bit flip in every third
+        buf[offs[i] + int(lens[i]) - 7] ^= 0x10
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    desc["offset"] = offs.astype(np.uint32)
+    desc["len"] = lens
+    want = oracle.rx_chunk(buf, desc, 0)
+    assert (want["verdict"] == 9).sum() >= n // 3 - 1 and (want["verdict"] == 0).sum() >= n // 2
+    with gpu.Context(0) as ctx:
+        assert_same(run_rx_dev(ctx, buf, desc, 0), want, "max-length chunk")
+        b = to_dev(buf)
+        ptrs = torch.from_numpy(offs + b.data_ptr()).to(DEV)
+        lt = torch.from_numpy(lens.view(np.int16).copy()).to(DEV)
+        out = dev_results(n)
+        ctx.rx_ptrs_dev(ptrs, lt, n, out)
+        torch.cuda.synchronize()
+    assert_same(out.cpu().numpy().view(RESULT_DTYPE), want, "max-length pointers")
