@@ -385,6 +385,9 @@ int main(int argc, char **argv) {
         vs.push_back({"sorted_cu2", rx_kernel<kRxChunk, false, 4>, 2});
         vs.push_back({"sorted6_cu2", rx_kernel<kRxChunk, false, 6>, 2});
         vs.push_back({"abl1_unrolled_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0>, 2});
+        vs.push_back({"abl1_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 1>, 2});
+        vs.push_back({"abl2_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 2>, 2});
+        vs.push_back({"abl3_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 3>, 2});
         if (strcmp(cfg, "c2") == 0) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
             vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
