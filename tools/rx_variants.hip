@@ -402,6 +402,8 @@ int main(int argc, char **argv) {
         // tx fill last: it repairs the corrupted frames the rx variants compare on
         vs.push_back({"tx_unrolled_cu2", rx_kernel<kTxChunk, false, 3>, 2});
         vs.push_back({"tx_unrolled_nodefer_cu2", rx_kernel<kTxChunk, false, 3, false, 0, 0>, 2});
+        vs.push_back({"tx_unrolled_nodefer_temporal_cu2", rx_kernel<kTxChunk, false, 3, false, 0, 0, 8, false>, 2});
+        vs.push_back({"tx_unrolled_temporal_cu2", rx_kernel<kTxChunk, false, 3, false, 0, 8, 8, false>, 2});
     }
     if (single) vs.resize(1);
     hipEvent_t a, b;
