@@ -145,11 +145,10 @@ void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
 }
 
 template <int MODE, bool RSS>
-void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
+void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, uint64_t slot) {
     if constexpr (MODE == mg::kRxPtrs) {
         launch_one<MODE, RSS, 3, true>(grid, block, st, kp);      // pointers: any frame size
     } else {
-        const uint64_t slot = kp.buf_len / kp.n;
         if (slot < kUnrollBelowSlotBytes)
             launch_one<MODE, RSS, 6, false>(grid, block, st, kp);
         else if (slot > kLineAlignAboveSlotBytes)
@@ -159,15 +158,35 @@ void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) 
     }
 }
 
+// A wave holds its results for up to kHeldPasses passes and stores them in
+// one burst at the end (rx_kernel DEFER); a batch needing more passes would
+// flush mid-stream, which costs more than a second launch (C4's 2 M x 1500 B
+// per GPU: one launch 511 us, two launches of 1 M ~486 us).  So a batch is
+// cut into launches of at most grid x 4 waves x 64 x kHeldPasses packets.
+constexpr uint32_t kHeldPasses = 8;
+
 template <int MODE>
 int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     if (kp.n == 0) return MTCP_GPU_OK;
     const dim3 grid(grid_for(ctx, kp.n)), block(mg::kBlock);
     const bool rss = MODE != mg::kTxChunk && (ctx->flags & MTCP_GPU_F_RSS);
-    if (rss)
-        launch_sched<MODE, true>(grid, block, st, kp);
-    else
-        launch_sched<MODE, false>(grid, block, st, kp);
+    const uint64_t slot = kp.n ? kp.buf_len / kp.n : 0;       // the whole batch's average slot
+    const uint32_t cap = grid.x * mg::kWavesPerBlock * mg::kWave * kHeldPasses;
+    for (uint32_t first = 0; first < kp.n; first += cap) {
+        mg::KParams sub = kp;
+        sub.n = std::min(kp.n - first, cap);
+        if (MODE == mg::kRxPtrs) {
+            sub.ptrs = kp.ptrs + first;
+            sub.lens = kp.lens + first;
+        } else {
+            sub.desc = kp.desc + first;
+        }
+        if (MODE != mg::kTxChunk) sub.out = kp.out + first;
+        if (rss)
+            launch_sched<MODE, true>(grid, block, st, sub, slot);
+        else
+            launch_sched<MODE, false>(grid, block, st, sub, slot);
+    }
     return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
 

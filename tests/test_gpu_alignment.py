@@ -120,3 +120,30 @@ def test_maximum_length_frames(gpu):
         ctx.rx_ptrs_dev(ptrs, lt, n, out)
         torch.cuda.synchronize()
     assert_same(out.cpu().numpy().view(RESULT_DTYPE), want, "max-length pointers")
+
+
+def test_batches_larger_than_one_launch(gpu):
+    """Batches beyond one launch's held passes (mtcp_gpu.hip launch: grid x 4
+    waves x 64 x 8 packets, 1 M on a full MI355X) are cut into several
+    launches; every record of every launch, the pointer-burst twin and the tx
+    fill must still equal the oracle's."""
+    n, seed = (1 << 20) + 4099, 31
+    desc, nbytes = pktgen.layout(n, 64, 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(None, 8, 1))
+    with gpu.Context(0, rss=True, rss_queues=8) as ctx:
+        assert_same(run_rx_dev(ctx, buf, desc, 6), want, "split chunk")
+        b = to_dev(buf)
+        ptrs = torch.from_numpy((desc["offset"].astype(np.int64) << 6) + b.data_ptr()).to(DEV)
+        lens = torch.from_numpy(desc["len"].view(np.int16).copy()).to(DEV)
+        out = dev_results(n)
+        ctx.rx_ptrs_dev(ptrs, lens, n, out)
+        torch.cuda.synchronize()
+        assert_same(out.cpu().numpy().view(RESULT_DTYPE), want, "split pointers")
+        ctx.tx_fill_dev(b, to_dev(desc), n, 6)
+        torch.cuda.synchronize()
+    fixed = buf.copy()
+    oracle.tx_fill(fixed, desc, 6)
+    assert not np.array_equal(fixed, buf)                  # the batch has corrupted frames
+    assert np.array_equal(b.cpu().numpy(), fixed)
