@@ -336,14 +336,26 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if world > 1:
+        # A barrier releases the ranks up to a few hundred µs apart, which a
+        # short timed region (K x 0.24 ms) would count as lost scaling.  The
+        # ranks share one host and so one CLOCK_MONOTONIC (perf_counter):
+        # after the barrier they agree on a start instant 5 ms past the
+        # latest rank's clock and spin until it; each rank's time runs from
+        # that common instant (a rank arriving late is charged for it).
+        tt = torch.tensor([t0], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t0 = float(tt[0]) + 5e-3
+        while time.perf_counter() < t0:
+            pass
     ev0.record(stream)
     for _ in range(args.steps):
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
+    t1 = time.perf_counter()     # this rank's completion; the max over ranks is taken below
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
     elapsed = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
