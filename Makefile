@@ -38,7 +38,13 @@ tools/rx_variants: tools/rx_variants.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
 tools/hbm_ceiling: tools/hbm_ceiling.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -w -o $@ $<
 
-tools: tools/rx_variants tools/hbm_ceiling
+tools/store_probe: tools/store_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -w -o $@ $<
+
+tools/pcie_probe: tools/pcie_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -w -o $@ $<
+
+tools: tools/rx_variants tools/hbm_ceiling tools/store_probe tools/pcie_probe
 
 # gpu_module.c driven by the RunMainLoop rx harness; the
 # mTCP types come from the test doubles in tests/c/mtcp_double.
