@@ -126,7 +126,7 @@ uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
 // pre-issued first large round, through L2 (SCHED 6): a 64 B frame shares its
 // 128 B line with a neighbour's edge that another round streams, and the
 // early temporal load lets that round hit it (C3 140.7 -> 134.3 us).
-// Pointer bursts have no chunk size: unrolled.
+// Pointer bursts have no chunk size: sorted (see launch_sched).
 // Frames longer than one trip (1536 B) are streamed from the start of their
 // first 128 B line (rx_kernel LALIGN) so that no trip boundary splits a line:
 // C5's 9024 B slots put every other frame off the line grid, and without it
@@ -147,7 +147,11 @@ void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
 template <int MODE, bool RSS>
 void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, uint64_t slot) {
     if constexpr (MODE == mg::kRxPtrs) {
-        launch_one<MODE, RSS, 3, true>(grid, block, st, kp);      // pointers: any frame size
+        // pointer bursts carry no size hint the host can see (the lengths are
+        // in device memory): the size-sorted rounds are the robust choice —
+        // C3-shaped bursts 135.5 vs 162.1 us unrolled, C2-shaped 250.5 vs
+        // 245.3, C5-shaped 687.7 vs 685.2 (tools/rx_variants ptrs_*)
+        launch_one<MODE, RSS, 6, true>(grid, block, st, kp);
     } else {
         if (slot < kUnrollBelowSlotBytes)
             launch_one<MODE, RSS, 6, false>(grid, block, st, kp);

@@ -355,6 +355,23 @@ int main(int argc, char **argv) {
     kp.rss_tables = d_tab;
     kp.rss_nq = 8;
     kp.rss_endian = 1;
+    // the same frames as a pointer burst (DPDK-style): ptrs[i] = buf + offset
+    {
+        std::vector<uint64_t> hp(n);
+        std::vector<uint16_t> hl(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            hp[i] = (uint64_t)(uintptr_t)d_buf + ((uint64_t)desc[i].offset << 6);
+            hl[i] = desc[i].len;
+        }
+        uint64_t *dp;
+        uint16_t *dl;
+        CK(hipMalloc(&dp, n * 8));
+        CK(hipMalloc(&dl, n * 2));
+        CK(hipMemcpy(dp, hp.data(), n * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(dl, hl.data(), n * 2, hipMemcpyHostToDevice));
+        kp.ptrs = reinterpret_cast<const uint8_t *const *>(dp);
+        kp.lens = dl;
+    }
 
     std::vector<Variant> vs;
     using namespace mg;
@@ -362,6 +379,8 @@ int main(int argc, char **argv) {
         // variant 0 = what mtcp_gpu.hip dispatches for C3; every other variant's
         // records must equal its records byte for byte
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
+        vs.push_back({"ptrs_rss_unrolled_lalign_cu2", rx_kernel<kRxPtrs, true, 3, true>, 2});
+        vs.push_back({"ptrs_rss_sorted6_lalign_cu2", rx_kernel<kRxPtrs, true, 6, true>, 2});
         vs.push_back({"rss_rolled_cu2", rx_kernel<kRxChunk, true, 0>, 2});
         vs.push_back({"rss_unrolled_cu2", rx_kernel<kRxChunk, true, 3>, 2});
         vs.push_back({"rss_sorted_cu2", rx_kernel<kRxChunk, true, 4>, 2});
@@ -377,6 +396,8 @@ int main(int argc, char **argv) {
         // variant 0 = what mtcp_gpu.hip dispatches for C2 (C5 adds LALIGN)
         vs.push_back({"unrolled_cu2", rx_kernel<kRxChunk, false, 3>, 2});
         vs.push_back({"unrolled_lalign_cu2", rx_kernel<kRxChunk, false, 3, true>, 2});
+        vs.push_back({"ptrs_unrolled_lalign_cu2", rx_kernel<kRxPtrs, false, 3, true>, 2});
+        vs.push_back({"ptrs_sorted6_lalign_cu2", rx_kernel<kRxPtrs, false, 6, true>, 2});
         vs.push_back({"rolled_cu2", rx_kernel<kRxChunk, false, 0>, 2});
         vs.push_back({"rolled_lalign_cu2", rx_kernel<kRxChunk, false, 0, true>, 2});
         vs.push_back({"unrolled_cu3", rx_kernel<kRxChunk, false, 3>, 3});
