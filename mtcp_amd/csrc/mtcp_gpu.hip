@@ -151,14 +151,14 @@ void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, 
         // in device memory): the size-sorted rounds are the robust choice —
         // C3-shaped bursts 135.5 vs 162.1 us unrolled, C2-shaped 250.5 vs
         // 245.3, C5-shaped 687.7 vs 685.2 (tools/rx_variants ptrs_*)
-        launch_one<MODE, RSS, 6, true>(grid, block, st, kp);
+        launch_one<MODE, RSS, mg::kSchedSorted, true>(grid, block, st, kp);
     } else {
         if (slot < kUnrollBelowSlotBytes)
-            launch_one<MODE, RSS, 6, false>(grid, block, st, kp);
+            launch_one<MODE, RSS, mg::kSchedSorted, false>(grid, block, st, kp);
         else if (slot > kLineAlignAboveSlotBytes)
-            launch_one<MODE, RSS, 3, true>(grid, block, st, kp);
+            launch_one<MODE, RSS, mg::kSchedUnrolled, true>(grid, block, st, kp);
         else
-            launch_one<MODE, RSS, 3, false>(grid, block, st, kp);
+            launch_one<MODE, RSS, mg::kSchedUnrolled, false>(grid, block, st, kp);
     }
 }
 

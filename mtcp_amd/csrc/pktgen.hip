@@ -136,7 +136,7 @@ extern "C" int mtcp_gpu_pktgen_dev(void *d_buf, uint64_t buf_len, const mtcp_gpu
     kp.off_shift = off_shift;
     const uint32_t groups = (n + 63) / 64;
     const uint32_t fill_blocks = (groups + 3) / 4 < 2048 ? (groups + 3) / 4 : 2048;
-    hipLaunchKernelGGL((mg::rx_kernel<mg::kTxChunk, false, 3, true>), dim3(fill_blocks), dim3(256), 0, st, kp);
+    hipLaunchKernelGGL((mg::rx_kernel<mg::kTxChunk, false, mg::kSchedUnrolled, true>), dim3(fill_blocks), dim3(256), 0, st, kp);
     hipLaunchKernelGGL(gen_corrupt, dim3(lane_blocks), dim3(256), 0, st, gp);
     return hipGetLastError() == hipSuccess ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }

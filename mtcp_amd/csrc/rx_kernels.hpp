@@ -48,6 +48,15 @@ constexpr int kRow = 16;                 // lanes per DPP row = lanes per frame
 constexpr int kUnroll = 6;               // loads in flight per row (96 chunks = 1536 B)
 
 enum Mode : int { kRxChunk = 0, kRxPtrs = 1, kTxChunk = 2 };
+// Phase-1 schedules (rx_kernel's SCHED; see its comment).  Dispatched:
+// kSchedUnrolled and kSchedSorted; the others are A/B baselines.
+enum Sched : int {
+    kSchedRolled = 0,        // rolled trip loop
+    kSchedUnrolled = 3,      // 16 rounds unrolled, single-buffered
+    kSchedSortedBase = 4,    // size-sorted rounds
+    kSchedSortedEarly = 5,   // + first small rounds with the first large round
+    kSchedSorted = 6,        // + issued with the previous pass's pre-issue
+};
 
 struct KParams {
     const uint8_t *buf;            // chunk base (chunk modes), 16 B aligned
