@@ -16,6 +16,7 @@
 
 #include "../../include/mtcp_gpu.h"
 #include "flow_kernels.hpp"
+#include "host_copy.hpp"
 #include "rx_kernels.hpp"
 
 namespace {
@@ -502,10 +503,11 @@ int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16
         d.offset = (uint32_t)(off >> 6);
         d.len = lens[i];
         d.flags = d.rsvd = 0;
-        if (pkts[i]) memcpy(ctx->h_gather + off, pkts[i], lens[i]);
+        if (pkts[i]) stage_copy(ctx->h_gather + off, pkts[i], lens[i]);
         else d.len = 0xFFFF, d.offset = 0xFFFFFFFFu;   // -> BAD_DESC
         off += ((uint64_t)lens[i] + 63) & ~63ull;
     }
+    stage_fence();
     return mtcp_gpu_rx_chunk(ctx, ctx->h_gather, total, ctx->h_gather_desc, n, 6, out);
 }
 

@@ -7,12 +7,11 @@
 #include <stdint.h>
 #include <string.h>
 
-#include <emmintrin.h>
-
 #include <new>
 
 #include "../../include/mtcp_gpu.h"
 #include "../../include/mtcp_gpu_rxq.h"
+#include "host_copy.hpp"
 
 struct mtcp_gpu_rxq {
     mtcp_gpu_ctx *ctx = nullptr;
@@ -25,32 +24,6 @@ struct mtcp_gpu_rxq {
     uint32_t done = 0;                   // frames with results
     uint64_t used = 0;                   // staging bytes in use
 };
-
-// Copy a frame into its 64 B-aligned staging slot with streaming stores:
-// the slot is read next by the DMA engine, not by this core, so the stores
-// skip the read-for-ownership of a normal memcpy.  The slot's tail up to the
-// next 16 B is written too (it belongs to the slot's padding).
-static void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t len) {
-    uint32_t i = 0;
-    for (; i + 64 <= len; i += 64) {
-        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i));
-        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 16));
-        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 32));
-        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 48));
-        _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), a);
-        _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 16), b);
-        _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 32), c);
-        _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 48), d);
-    }
-    for (; i + 16 <= len; i += 16)
-        _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i),
-                         _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i)));
-    if (i < len) {                        // last partial 16 B: through a bounce buffer
-        alignas(16) uint8_t t[16] = {0};
-        memcpy(t, src + i, len - i);
-        _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), _mm_load_si128(reinterpret_cast<const __m128i *>(t)));
-    }
-}
 
 extern "C" {
 
@@ -115,7 +88,7 @@ int mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n) {
     if (!q) return MTCP_GPU_EINVAL;
     int rc = MTCP_GPU_OK;
     if (q->n > q->done) {
-        _mm_sfence();                     // the streaming stores of rxq_push are visible to the DMA
+        stage_fence();                    // the streaming stores of rxq_push are visible to the DMA
         // frames staged after the last flush: their descriptors are relative
         // to the staging base, so the whole chunk prefix is handed over
         rc = mtcp_gpu_rx_chunk(q->ctx, q->buf, q->used, q->desc + q->done, q->n - q->done, 6,
