@@ -5,8 +5,11 @@
 // (mtcp/src/tcp_util.c:157-190), the Toeplitz RSS hash (util/rss.c:107-165),
 // and the tx checksum fill (ip_out.c:94,164; tcp_out.c:211,329).
 //
-// Work decomposition: one 64-lane wave per group of 64 consecutive packets;
-// lane k owns packet k of the group.
+// Work decomposition: one 64-lane wave per group of 64 packets (interleaved
+// over the grid in runs of B = 8); lane k owns packet k of the group.  The
+// phase-1 round order depends on the schedule (SCHED, below): the 16 rounds
+// in frame order for large frames, size-sorted rounds (large frames four
+// per round, small ones sixteen per round) for mixed or small ones.
 //   phase 0  lane k loads its descriptor (one coalesced 8-byte load); no
 //            header is read yet.
 //   phase 1  the four 16-lane DPP rows of the wave stream four frames at a
@@ -21,7 +24,10 @@
 //            checksum), subtracts from the chunk sum the bytes outside the
 //            TCP segment [T, E) (E = 14 + tot_len), adds the pseudo header,
 //            folds, hashes the 4-tuple through 24 nibble tables in LDS and
-//            stores its record (staged in LDS, written as whole 16 B lanes).
+//            holds its 40 B record in registers; the held records of up to
+//            8 passes are stored at the end (through LDS, as 16 B pieces of
+//            contiguous runs) — stores interleaved with the frame stream
+//            cost several times their bytes.
 // HBM traffic is one pass over the frames plus descriptors and results.
 // Exactness: the reference sums little-endian u16 words into a u32 (no
 // overflow for any u16 length).  Every packet starts at an even address, so
