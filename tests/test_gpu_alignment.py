@@ -147,3 +147,44 @@ def test_batches_larger_than_one_launch(gpu):
     oracle.tx_fill(fixed, desc, 6)
     assert not np.array_equal(fixed, buf)                  # the batch has corrupted frames
     assert np.array_equal(b.cpu().numpy(), fixed)
+
+
+@pytest.mark.parametrize("size,n", [(1500, 150000), ("bimodal", 300000), (9000, 20000)])
+def test_host_pipeline_stages_match_device_path(gpu, size, n):
+    """mtcp_gpu_rx_chunk on a host chunk far larger than one pipeline stage
+    (64 MiB or 64 K descriptors, three streams): every record equals the
+    device path's on the same frames, and a sample equals the oracle's."""
+    seed = 41
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    d = to_dev(desc)
+    gpu.pktgen_dev(b, d, n, 6, seed)
+    out = dev_results(n)
+    with gpu.Context(0, rss=True, rss_queues=5) as ctx:
+        ctx.rx_chunk_dev(b, d, n, 6, out)
+        torch.cuda.synchronize()
+        dev = out.cpu().numpy().view(RESULT_DTYPE)
+        host = b.cpu().numpy()
+        got = ctx.rx_chunk(host, desc, 6)
+    assert nbytes > 2 * (64 << 20) or n > 2 * (1 << 16)
+    assert_same(got, dev, f"host pipeline {size}")
+    idx = np.sort(np.random.default_rng(1).choice(n, size=2000, replace=False))
+    assert_same(got[idx], oracle.rx_chunk(host, desc[idx], 6, oracle.rss_cfg(None, 5, 1)), "sample")
+
+
+def test_rss_queue_every_nq_and_endian(gpu):
+    """GetRSSCPUCore for every queue count mTCP can run (1..16, MAX_CPUS) with
+    and without the endian fix (mtcp/src/rss.c:90-103), both keys, on one
+    bimodal batch: rss_hash and rss_queue of every packet equal the oracle's."""
+    n, seed = 1 << 13, 43
+    desc, nbytes = pktgen.layout(n, "bimodal", 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    for key in (None, oracle.KEY_MICROSOFT):
+        for nq in range(1, 17):
+            for endian in (0, 1):
+                want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(key, nq, endian))
+                with gpu.Context(0, rss=True, rss_key=key, rss_queues=nq, rss_endian=bool(endian)) as ctx:
+                    got = run_rx_dev(ctx, buf, desc, 6)
+                assert np.array_equal(got["rss_hash"], want["rss_hash"]), (nq, endian)
+                assert np.array_equal(got["rss_queue"], want["rss_queue"]), (nq, endian)
