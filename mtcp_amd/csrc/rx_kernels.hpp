@@ -185,6 +185,7 @@ struct Trip {
     uint64_t base;
     uint32_t col;     // the frame's owner lane = its column in WaveLds (kWave: scratch)
     uint32_t skip = 0;  // LALIGN: chunks before the frame at the start of the first trip
+    uint32_t k = 0, ntrip = 0;   // REV: trip step and the frame's trip count
 };
 
 // Packet <-> lane mapping, in passes of 64*W packets (W = waves in the grid):
@@ -210,7 +211,7 @@ struct Trip {
 // with the next pass's loads — lost on every config and were removed).
 // LALIGN: multi-trip frames stream from the start of their first 128 B line.
 template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
-          bool NT = true, int U = 6>
+          bool NT = true, int U = 6, bool REV = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ WaveLds lds[kWavesPerBlock];
@@ -305,6 +306,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         t.base = ((uint64_t)row_bcast(f.r_hi, ii) << 32) | row_bcast(f.r_lo, ii);
         t.c0 = 0;
         line_align(t);
+        if constexpr (REV) {
+            // odd rows walk their frame's trips last to first, so that the
+            // line a frame shares with its neighbour in the next row is read
+            // by both rows in the same step (3 of every 4 frame boundaries)
+            t.k = 0;
+            t.ntrip = (t.nj + U * kRow - 1) / (U * kRow);
+            if ((row & 1) && t.ntrip > 1) t.c0 = (t.ntrip - 1) * (U * kRow);
+        }
+    };
+    auto rev_step = [&](Trip &t) {     // REV: the next trip of each row
+        ++t.k;
+        t.c0 = t.k >= t.ntrip ? t.nj                           // done: every lane masked
+               : (row & 1) ? (t.ntrip - 1 - t.k) * (U * kRow) : t.k * (U * kRow);
     };
     // next trip with work; false (nj = 0, base kept valid) when the pass is done
     auto advance = [&](const Frame &f, Trip &t) -> bool {
@@ -646,10 +660,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                 enter_round(f, t, i);
                 if (i > 0 || !have_pre) issue(t, X);
                 consume(t, X, acc);
-                while (__ballot(t.c0 + U * kRow < t.nj)) {
-                    t.c0 += U * kRow;
-                    issue(t, X);
-                    consume(t, X, acc);
+                if constexpr (REV) {
+                    while (__ballot(t.k + 1 < t.ntrip)) {
+                        rev_step(t);
+                        issue(t, X);
+                        consume(t, X, acc);
+                    }
+                } else {
+                    while (__ballot(t.c0 + U * kRow < t.nj)) {
+                        t.c0 += U * kRow;
+                        issue(t, X);
+                        consume(t, X, acc);
+                    }
                 }
                 acc = row_sum(acc);
                 if (rlane == kRow - 1) wl.sum[4 * i + (int)row] = acc;

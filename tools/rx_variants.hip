@@ -396,6 +396,7 @@ int main(int argc, char **argv) {
         // variant 0 = what mtcp_gpu.hip dispatches for C2 (C5 adds LALIGN)
         vs.push_back({"unrolled_cu2", rx_kernel<kRxChunk, false, 3>, 2});
         vs.push_back({"unrolled_lalign_cu2", rx_kernel<kRxChunk, false, 3, true>, 2});
+        vs.push_back({"unrolled_lalign_rev_cu2", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true>, 2});
         vs.push_back({"ptrs_unrolled_lalign_cu2", rx_kernel<kRxPtrs, false, 3, true>, 2});
         vs.push_back({"ptrs_sorted6_lalign_cu2", rx_kernel<kRxPtrs, false, 6, true>, 2});
         vs.push_back({"rolled_cu2", rx_kernel<kRxChunk, false, 0>, 2});
