@@ -176,6 +176,16 @@ int  mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key,
                    int rss_num_queues, uint32_t flags);
 void mtcp_gpu_close(mtcp_gpu_ctx *ctx);
 
+/*
+ * Optional, at init time (an io_module's init_handle): allocate the device
+ * staging that host-buffer calls (mtcp_gpu_rx_chunk, _rx_ptrs, _tx_fill) of
+ * up to `max_bytes` chunk bytes and `max_pkts` frames use, and load the
+ * kernels, so that the first call on the data path pays for neither
+ * (otherwise both happen lazily on the first call).  MTCP_GPU_ENOMEM if the
+ * device memory is not there.
+ */
+int  mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts);
+
 /* dev_ioctl-compatible capability answer (0 = offloaded, -1 = software). */
 int  mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp);
 

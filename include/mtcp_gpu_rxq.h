@@ -11,7 +11,7 @@
  * receive (psio_module.c:244-246, dpdk_module.c:395-398).  An rxq therefore
  * copies the frames of several bursts into pinned staging laid out like a
  * PSIO chunk (64 B aligned, io_engine/lib/pslib.c:146), runs the rx kernel
- * over the aggregate once (mtcp_gpu_rx_chunk), and then answers get_rptr
+ * over the aggregate once (mtcp_gpu_rx_chunk_dev), and then answers get_rptr
  * from the staging copy:
  *
  *   - MTCP_GPU_V_IP_CSUM_BAD, MTCP_GPU_V_TCP_CSUM_BAD -> NULL, exactly the
@@ -59,6 +59,16 @@ uint32_t mtcp_gpu_rxq_pending(const mtcp_gpu_rxq *q);
 /* Run the rx kernel over everything staged since the last reset; *n = the
  * number of frames now served by mtcp_gpu_rxq_get (synchronous). */
 int  mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n);
+
+/* The same in two halves, so that a backend can overlap the GPU with its
+ * own work (gpu_module.c serves aggregate k while k+1 is checked):
+ * flush_async starts the rx kernel over the frames staged since the last
+ * flush (one H2D of frames + descriptors, the kernel, one D2H of results, on
+ * the rxq's own stream) and returns; until rxq_wait the rxq takes no pushes,
+ * flushes or resets (MTCP_GPU_EINVAL).  rxq_wait blocks until the results
+ * are in and then behaves like the end of rxq_flush. */
+int  mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q);
+int  mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n);
 
 /* get_rptr for flushed frame i: the staged frame and its length, or NULL for
  * the checksum failures listed above.  *res (may be NULL) receives the

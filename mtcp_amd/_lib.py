@@ -14,13 +14,13 @@ LIB_PATH = os.path.join(HERE, "lib", "libmtcp_gpu.so")
 # Every symbol include/mtcp_gpu.h and include/mtcp_gpu_pktgen.h declare.
 EXPORTS = (
     "mtcp_gpu_abi_version", "mtcp_gpu_strerror", "mtcp_gpu_device_count", "mtcp_gpu_open",
-    "mtcp_gpu_close", "mtcp_gpu_dev_ioctl", "mtcp_gpu_stream", "mtcp_gpu_rx_chunk_dev",
+    "mtcp_gpu_close", "mtcp_gpu_reserve", "mtcp_gpu_dev_ioctl", "mtcp_gpu_stream", "mtcp_gpu_rx_chunk_dev",
     "mtcp_gpu_rx_ptrs_dev", "mtcp_gpu_rx_chunk", "mtcp_gpu_rx_ptrs", "mtcp_gpu_tx_fill_dev",
     "mtcp_gpu_tx_fill", "mtcp_gpu_host_register", "mtcp_gpu_host_unregister", "mtcp_gpu_sync",
     "mtcp_gpu_flow_hash_dev", "mtcp_gpu_flow_hash", "mtcp_gpu_rss_queue_map_dev",
     "mtcp_gpu_addr_pool_search", "mtcp_gpu_pktgen_dev",
     "mtcp_gpu_rxq_create", "mtcp_gpu_rxq_destroy", "mtcp_gpu_rxq_push", "mtcp_gpu_rxq_push_chunk",
-    "mtcp_gpu_rxq_pending", "mtcp_gpu_rxq_flush", "mtcp_gpu_rxq_get", "mtcp_gpu_rxq_frame", "mtcp_gpu_rxq_reset",
+    "mtcp_gpu_rxq_pending", "mtcp_gpu_rxq_flush", "mtcp_gpu_rxq_flush_async", "mtcp_gpu_rxq_wait", "mtcp_gpu_rxq_get", "mtcp_gpu_rxq_frame", "mtcp_gpu_rxq_reset",
 )
 
 _lib = None
@@ -50,6 +50,7 @@ def lib() -> ctypes.CDLL:
         "mtcp_gpu_device_count": ([], i32),
         "mtcp_gpu_open": ([ctypes.POINTER(vp), i32, vp, i32, u32], i32),
         "mtcp_gpu_close": ([vp], None),
+        "mtcp_gpu_reserve": ([vp, u64, u32], i32),
         "mtcp_gpu_dev_ioctl": ([vp, i32, i32, vp], i32),
         "mtcp_gpu_stream": ([vp], vp),
         "mtcp_gpu_sync": ([vp], i32),
@@ -74,6 +75,8 @@ def lib() -> ctypes.CDLL:
         "mtcp_gpu_rxq_push_chunk": ([vp, vp, vp, u32, u32], i32),
         "mtcp_gpu_rxq_pending": ([vp], u32),
         "mtcp_gpu_rxq_flush": ([vp, ctypes.POINTER(u32)], i32),
+        "mtcp_gpu_rxq_flush_async": ([vp], i32),
+        "mtcp_gpu_rxq_wait": ([vp, ctypes.POINTER(u32)], i32),
         "mtcp_gpu_rxq_get": ([vp, u32, ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(vp)], vp),
         "mtcp_gpu_rxq_frame": ([vp, u32, ctypes.POINTER(ctypes.c_uint16)], vp),
         "mtcp_gpu_rxq_reset": ([vp], None),

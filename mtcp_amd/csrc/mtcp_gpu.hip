@@ -327,6 +327,28 @@ void mtcp_gpu_close(mtcp_gpu_ctx *ctx) {
     delete ctx;
 }
 
+int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
+    if (!ctx) return MTCP_GPU_EINVAL;
+    DeviceGuard dg(ctx->device);
+    if (!dg.ok) return MTCP_GPU_ENODEV;
+    // a host call's batches span at most kStageBytes / kStagePkts and start
+    // at stage 0; later stages are used only by calls larger than one stage
+    const uint64_t bytes = std::min(max_bytes, kStageBytes);
+    const uint32_t pkts = std::min(max_pkts, kStagePkts);
+    const int stages = max_bytes > kStageBytes || max_pkts > kStagePkts ? kStages : 1;
+    for (int i = 0; i < stages; ++i) {
+        const int rc = stage_reserve(ctx->stage[i], ((bytes + 15) & ~15ull) + 16, std::max(pkts, 1u));
+        if (rc != MTCP_GPU_OK) return rc;
+    }
+    // the code object loads on the first launch of any of its kernels
+    hipFuncAttributes attr;
+    if (!HIP_OK(hipFuncGetAttributes(
+            &attr, reinterpret_cast<const void *>(
+                       &mg::rx_kernel<mg::kRxChunk, false, mg::kSchedSorted, false, 0, 8, 8, true, 6, false>))))
+        return MTCP_GPU_EIO;
+    return MTCP_GPU_OK;
+}
+
 int mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp) {
     (void)nif;
     (void)argp;

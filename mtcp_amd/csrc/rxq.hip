@@ -1,8 +1,15 @@
 // rxq.hip — burst aggregation of include/mtcp_gpu_rxq.h: pinned PSIO-style
 // staging (64 B aligned frames, io_engine/lib/pslib.c:146) filled by the
-// io_module backend, one mtcp_gpu_rx_chunk over the aggregate, get_rptr
-// answered from the staging copy.  Host code only; the checksums run in
-// the rx kernel behind mtcp_gpu_rx_chunk.
+// io_module backend, one rx kernel launch over the aggregate, get_rptr
+// answered from the staging copy.  Host code only; the checksums run in the
+// rx kernel behind mtcp_gpu_rx_chunk_dev.
+//
+// Each rxq owns a device copy of its staging and a stream: a flush is one
+// H2D of [first frame, end of the descriptors) — the descriptors are copied
+// right behind the frames in the pinned buffer so that frames and
+// descriptors travel in one transfer — the kernel, and one D2H of the
+// results, so that flush_async / wait can overlap the GPU with the
+// backend's own work.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -15,15 +22,38 @@
 
 struct mtcp_gpu_rxq {
     mtcp_gpu_ctx *ctx = nullptr;
-    uint8_t *buf = nullptr;              // pinned staging chunk
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint8_t *buf = nullptr;              // pinned staging: frames, then room for descriptors
     mtcp_gpu_desc *desc = nullptr;       // pinned
     mtcp_gpu_result *res = nullptr;      // pinned
+    uint8_t *d_buf = nullptr;            // device copy of buf
+    mtcp_gpu_result *d_out = nullptr;
     uint32_t max_pkts = 0;
     uint64_t max_bytes = 0;
     uint32_t n = 0;                      // frames staged
     uint32_t done = 0;                   // frames with results
+    uint32_t inflight = 0;               // frames of an unfinished flush_async (0: none)
     uint64_t used = 0;                   // staging bytes in use
 };
+
+namespace {
+
+// the rxq's device is current for one call; the caller's is restored
+struct RxqDevice {
+    int prev = -1;
+    bool ok = false;
+    explicit RxqDevice(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = prev == device || hipSetDevice(device) == hipSuccess;
+    }
+    ~RxqDevice() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
 
 extern "C" {
 
@@ -31,18 +61,45 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
                         uint64_t max_bytes) {
     if (!out || !ctx || !max_pkts || max_bytes < 64) return MTCP_GPU_EINVAL;
     *out = nullptr;
+    hipDevice_t dev = 0;
+    if (hipStreamGetDevice(reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx)), &dev) != hipSuccess)
+        return MTCP_GPU_ENODEV;
+    RxqDevice dg(dev);
+    if (!dg.ok) return MTCP_GPU_ENODEV;
     mtcp_gpu_rxq *q = new (std::nothrow) mtcp_gpu_rxq;
     if (!q) return MTCP_GPU_ENOMEM;
     q->ctx = ctx;
+    q->device = dev;
     q->max_pkts = max_pkts;
     q->max_bytes = (max_bytes + 63) & ~63ull;
-    if (hipHostMalloc(&q->buf, q->max_bytes, hipHostMallocDefault) != hipSuccess ||
+    const uint64_t staging = q->max_bytes + (uint64_t)max_pkts * sizeof(mtcp_gpu_desc);
+    if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(&q->buf, staging, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&q->desc, (size_t)max_pkts * sizeof(mtcp_gpu_desc), hipHostMallocDefault) !=
             hipSuccess ||
         hipHostMalloc(&q->res, (size_t)max_pkts * sizeof(mtcp_gpu_result), hipHostMallocDefault) !=
-            hipSuccess) {
+            hipSuccess ||
+        hipMalloc(&q->d_buf, staging) != hipSuccess ||
+        hipMalloc(&q->d_out, (size_t)max_pkts * sizeof(mtcp_gpu_result)) != hipSuccess) {
         mtcp_gpu_rxq_destroy(q);
         return MTCP_GPU_ENOMEM;
+    }
+    // load the kernels and bring up the stream's copy queues (created on
+    // first use: the first H2D of a stream took 7.8 ms) now, not on the
+    // first flush of the data path
+    // (copies the size of a flush's: small ones take another path)
+    int rc = mtcp_gpu_reserve(ctx, 0, 0);
+    const uint64_t h2d = staging < (1ull << 20) ? staging : (1ull << 20);
+    const uint64_t d2h = (uint64_t)max_pkts * sizeof(mtcp_gpu_result);
+    memset(q->buf, 0, h2d);
+    if (rc == MTCP_GPU_OK &&
+        (hipMemcpyAsync(q->d_buf, q->buf, h2d, hipMemcpyHostToDevice, q->stream) != hipSuccess ||
+         hipMemcpyAsync(q->res, q->d_out, d2h, hipMemcpyDeviceToHost, q->stream) != hipSuccess ||
+         hipStreamSynchronize(q->stream) != hipSuccess))
+        rc = MTCP_GPU_EIO;
+    if (rc != MTCP_GPU_OK) {
+        mtcp_gpu_rxq_destroy(q);
+        return rc;
     }
     *out = q;
     return MTCP_GPU_OK;
@@ -50,15 +107,23 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
 
 void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q) {
     if (!q) return;
+    RxqDevice dg(q->device);
+    if (q->stream) {
+        (void)hipStreamSynchronize(q->stream);
+        (void)hipStreamDestroy(q->stream);
+    }
     if (q->buf) (void)hipHostFree(q->buf);
     if (q->desc) (void)hipHostFree(q->desc);
     if (q->res) (void)hipHostFree(q->res);
+    if (q->d_buf) (void)hipFree(q->d_buf);
+    if (q->d_out) (void)hipFree(q->d_out);
     delete q;
 }
 
 int mtcp_gpu_rxq_push(mtcp_gpu_rxq *q, const uint8_t *frame, uint16_t len) {
     if (!q || (!frame && len)) return MTCP_GPU_EINVAL;
     const uint64_t slot = ((uint64_t)len + 63) & ~63ull;
+    if (q->inflight) return MTCP_GPU_EINVAL;       // staging is being read by the GPU
     if (q->n == q->max_pkts || q->used + slot > q->max_bytes) return MTCP_GPU_ENOSPC;
     if (q->done) return MTCP_GPU_EINVAL;           // flushed frames not yet reset
     mtcp_gpu_desc &d = q->desc[q->n];
@@ -84,19 +149,59 @@ int mtcp_gpu_rxq_push_chunk(mtcp_gpu_rxq *q, const uint8_t *buf, const mtcp_gpu_
 
 uint32_t mtcp_gpu_rxq_pending(const mtcp_gpu_rxq *q) { return q ? q->n - q->done : 0; }
 
-int mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n) {
+int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
+    if (!q || q->inflight) return MTCP_GPU_EINVAL;
+    if (q->n == q->done) return MTCP_GPU_OK;
+    RxqDevice dg(q->device);
+    if (!dg.ok) return MTCP_GPU_ENODEV;
+    const uint32_t first = q->done, cnt = q->n - q->done;
+    // frames staged since the last flush: their descriptors are relative to
+    // the staging base; the descriptors go right behind the frames
+    const uint64_t lo = (uint64_t)q->desc[first].offset << 6;
+    const uint64_t dbytes = (uint64_t)cnt * sizeof(mtcp_gpu_desc);
+    memcpy(q->buf + q->used, q->desc + first, dbytes);
+    stage_fence();                        // rxq_push's streaming stores are visible to the DMA
+    if (hipMemcpyAsync(q->d_buf + lo, q->buf + lo, q->used - lo + dbytes, hipMemcpyHostToDevice,
+                       q->stream) != hipSuccess)
+        return MTCP_GPU_EIO;
+    int rc = mtcp_gpu_rx_chunk_dev(q->ctx, q->d_buf, q->used,
+                                   reinterpret_cast<const mtcp_gpu_desc *>(q->d_buf + q->used), cnt,
+                                   6, q->d_out, q->stream);
+    if (rc == MTCP_GPU_OK &&
+        hipMemcpyAsync(q->res + first, q->d_out, (size_t)cnt * sizeof(mtcp_gpu_result),
+                       hipMemcpyDeviceToHost, q->stream) != hipSuccess)
+        rc = MTCP_GPU_EIO;
+    if (rc != MTCP_GPU_OK) {
+        (void)hipStreamSynchronize(q->stream);
+        return rc;
+    }
+    q->inflight = cnt;
+    return MTCP_GPU_OK;
+}
+
+int mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n) {
     if (!q) return MTCP_GPU_EINVAL;
     int rc = MTCP_GPU_OK;
-    if (q->n > q->done) {
-        stage_fence();                    // the streaming stores of rxq_push are visible to the DMA
-        // frames staged after the last flush: their descriptors are relative
-        // to the staging base, so the whole chunk prefix is handed over
-        rc = mtcp_gpu_rx_chunk(q->ctx, q->buf, q->used, q->desc + q->done, q->n - q->done, 6,
-                               q->res + q->done);
-        if (rc == MTCP_GPU_OK) q->done = q->n;
+    if (q->inflight) {
+        RxqDevice dg(q->device);
+        if (hipStreamSynchronize(q->stream) == hipSuccess)
+            q->done += q->inflight;
+        else
+            rc = MTCP_GPU_EIO;
+        q->inflight = 0;
     }
     if (n) *n = q->done;
     return rc;
+}
+
+int mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n) {
+    if (!q) return MTCP_GPU_EINVAL;
+    const int rc = mtcp_gpu_rxq_flush_async(q);
+    if (rc != MTCP_GPU_OK) {
+        if (n) *n = q->done;
+        return rc;
+    }
+    return mtcp_gpu_rxq_wait(q, n);
 }
 
 uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
@@ -117,7 +222,7 @@ uint8_t *mtcp_gpu_rxq_frame(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len) {
 }
 
 void mtcp_gpu_rxq_reset(mtcp_gpu_rxq *q) {
-    if (!q) return;
+    if (!q || q->inflight) return;                 // a flush_async is reading the staging
     q->n = q->done = 0;
     q->used = 0;
 }

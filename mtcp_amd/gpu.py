@@ -66,6 +66,11 @@ class Context:
             lib().mtcp_gpu_close(self._h)
             self._h = ctypes.c_void_p()
 
+    def reserve(self, max_bytes: int, max_pkts: int) -> None:
+        """Allocate the host calls' device staging and load the kernels now
+        (mtcp_gpu_reserve), instead of on the first host-buffer call."""
+        check(lib().mtcp_gpu_reserve(self._h, max_bytes, max_pkts), "mtcp_gpu_reserve")
+
     def __enter__(self):
         return self
 

@@ -9,16 +9,23 @@
  * those as rx_errors) and whether a served frame is byte-identical to the
  * original; dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers are logged.
  *
- *   rxloop CHUNK DESC OUT [timing]
+ *   rxloop CHUNK DESC OUT [timing|verify] [THREADS]
  *     CHUNK  frame bytes; DESC mtcp_gpu_desc records (byte offsets)
  *     OUT    one byte per frame: 0 NULL, 1 served intact, 2 served but changed
  *     timing served frames are not compared (only their first 64 B are read,
  *            as ProcessPacket's parse would): the loop's rate without the
  *            harness's own byte-for-byte check
+ *     THREADS  mTCP threads (default 1), one per core as core.c:1057 runs
+ *            them: each has its own mtcp_thread_context (cpu = thread index),
+ *            so its own gpu_module context, GPU ctx and staging, and its own
+ *            backend over a contiguous shard of the frames (share-nothing);
+ *            the wall time runs from a common start barrier to the last
+ *            thread's end
  * Prints one JSON line with the counters and the wall time of the rx loop
  * (tools/io_path_bench.py turns that into the io_module path's rate).  Built with the test doubles in
  * tests/c/mtcp_double (two fields of mtcp_thread_context, io_module_func).
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -37,10 +44,10 @@ struct fake_psio {
     uint32_t n, next, base, cnt;
     int recv_calls;
 };
-static struct fake_psio g_fake;
+static __thread struct fake_psio *tl_fake;         /* this thread's backend */
 
 static void fake_load(void) {}
-static void fake_init(struct mtcp_thread_context *ctx) { ctx->io_private_context = &g_fake; }
+static void fake_init(struct mtcp_thread_context *ctx) { ctx->io_private_context = tl_fake; }
 static int32_t fake_link(struct mtcp_thread_context *ctx) { (void)ctx; return 0; }
 static void fake_release(struct mtcp_thread_context *ctx, int ifidx, unsigned char *p, int len)
 {
@@ -56,7 +63,7 @@ static int32_t fake_recv(struct mtcp_thread_context *ctx, int ifidx)
 {
     struct fake_psio *f = ctx->io_private_context;    /* must be the inner's */
     (void)ifidx;
-    if (f != &g_fake) { fprintf(stderr, "context swap broken\n"); exit(3); }
+    if (f != tl_fake) { fprintf(stderr, "context swap broken\n"); exit(3); }
     f->recv_calls++;
     f->base = f->next;
     f->cnt = f->n - f->next < 64 ? f->n - f->next : 64;
@@ -97,79 +104,150 @@ static void *slurp(const char *path, size_t *size)
     return p;
 }
 
-int main(int argc, char **argv)
+struct worker {
+    pthread_t tid;
+    int cpu, timing;
+    struct fake_psio fake;                 /* frames [first, first + fake.n) */
+    uint32_t first;
+    uint8_t *status;                       /* status + first */
+    uint64_t rx_packets, rx_errors, changed, hdr_sum;
+    int rounds, ioctl_ip, ioctl_tcp;
+    uint32_t seen;
+    struct timespec t1;
+};
+static pthread_barrier_t g_start;
+static struct timespec g_t0;
+
+static void *worker_main(void *arg)
 {
-    struct mtcp_thread_context ctx = {0, NULL};
-    size_t nb, nd;
-    uint8_t *status;
-    uint64_t rx_packets = 0, rx_errors = 0, changed = 0;
-    int rounds = 0, ioctl_ip = -2, ioctl_tcp = -2;
-    uint32_t seen = 0;
-    uint64_t frame_bytes = 0, hdr_sum = 0;
-    int timing;
-    struct timespec t0, t1;
-    double secs;
-    FILE *out;
+    struct worker *w = arg;
+    struct mtcp_thread_context ctx = {w->cpu, NULL};
+    const struct fake_psio *f = &w->fake;
 
-    if (argc < 4) { fprintf(stderr, "usage: rxloop CHUNK DESC OUT [timing]\n"); return 1; }
-    timing = argc > 4 && strcmp(argv[4], "timing") == 0;
-    g_fake.buf = slurp(argv[1], &nb);
-    g_fake.desc = slurp(argv[2], &nd);
-    g_fake.n = (uint32_t)(nd / sizeof(mtcp_gpu_desc));
-    status = calloc(g_fake.n + 1, 1);
-
-    gpu_inner_module = &fake_module;
-    gpu_module_func.load_module();
+    tl_fake = &w->fake;
+    w->ioctl_ip = w->ioctl_tcp = -2;
     gpu_module_func.init_handle(&ctx);
     gpu_module_func.link_devices(&ctx);
-    clock_gettime(CLOCK_MONOTONIC, &t0);
-    for (;;) {                                        /* core.c:763-777 */
+    if (pthread_barrier_wait(&g_start) == PTHREAD_BARRIER_SERIAL_THREAD)
+        clock_gettime(CLOCK_MONOTONIC, &g_t0);
+    pthread_barrier_wait(&g_start);                  /* g_t0 set before anyone runs */
+    for (int idle = 0;;) {                            /* core.c:763-777 */
         int32_t recv_cnt = gpu_module_func.recv_pkts(&ctx, 0), i;
-        if (recv_cnt <= 0)
-            break;
-        rounds++;
+        if (recv_cnt <= 0) {
+            /* mTCP polls on; the harness stops once its backend is drained
+             * and the module has returned nothing twice (a pipelined module
+             * returns 0 while it fills, and its last aggregate one call
+             * after the backend ran dry) */
+            if (f->next == f->n && ++idle >= 2)
+                break;
+            continue;
+        }
+        idle = 0;
+        w->rounds++;
         for (i = 0; i < recv_cnt; i++) {
             uint16_t len = 0;
             uint8_t *pktbuf = gpu_module_func.get_rptr(&ctx, 0, i, &len);
-            const mtcp_gpu_desc *d = &g_fake.desc[seen + (uint32_t)i];
+            const mtcp_gpu_desc *d = &f->desc[w->seen + (uint32_t)i];
             if (pktbuf != NULL) {
                 /* ProcessPacket(mtcp, rx_inf, ts, pktbuf, len) would run here */
-                if (timing) {
+                if (w->timing) {
                     /* timing mode: touch the headers as ProcessPacket's parse
                      * would (first 64 B), no byte-for-byte check */
                     uint32_t k;
-                    for (k = 0; k < 64 && k < len; k += 8) hdr_sum += pktbuf[k];
-                    status[seen + i] = 1;
+                    for (k = 0; k < 64 && k < len; k += 8) w->hdr_sum += pktbuf[k];
+                    w->status[w->seen + i] = 1;
                 } else {
-                    int same = len == d->len && memcmp(pktbuf, g_fake.buf + d->offset, len) == 0;
-                    status[seen + i] = same ? 1 : 2;
-                    changed += !same;
+                    int same = len == d->len && memcmp(pktbuf, f->buf + d->offset, len) == 0;
+                    w->status[w->seen + i] = same ? 1 : 2;
+                    w->changed += !same;
                 }
-                rx_packets++;
+                w->rx_packets++;
             } else {
-                rx_errors++;                           /* nstat.rx_errors[rx_inf]++ */
+                w->rx_errors++;                        /* nstat.rx_errors[rx_inf]++ */
             }
         }
-        if (ioctl_ip == -2) {
-            ioctl_ip = gpu_module_func.dev_ioctl(&ctx, 0, PKT_RX_IP_CSUM, NULL);
-            ioctl_tcp = gpu_module_func.dev_ioctl(&ctx, 0, PKT_RX_TCP_CSUM, NULL);
+        if (w->ioctl_ip == -2) {
+            w->ioctl_ip = gpu_module_func.dev_ioctl(&ctx, 0, PKT_RX_IP_CSUM, NULL);
+            w->ioctl_tcp = gpu_module_func.dev_ioctl(&ctx, 0, PKT_RX_TCP_CSUM, NULL);
         }
-        seen += (uint32_t)recv_cnt;
+        w->seen += (uint32_t)recv_cnt;
     }
-    clock_gettime(CLOCK_MONOTONIC, &t1);
+    clock_gettime(CLOCK_MONOTONIC, &w->t1);
     gpu_module_func.destroy_handle(&ctx);
-    for (uint32_t k = 0; k < g_fake.n; k++) frame_bytes += g_fake.desc[k].len;
+    return NULL;
+}
+
+int main(int argc, char **argv)
+{
+    size_t nb, nd;
+    uint8_t *status;
+    const uint8_t *buf;
+    const mtcp_gpu_desc *desc;
+    uint32_t n, seen = 0;
+    uint64_t rx_packets = 0, rx_errors = 0, changed = 0, hdr_sum = 0, frame_bytes = 0;
+    int rounds = 0, recv_calls = 0, timing, threads, t;
+    struct timespec t1;
+    struct worker *ws;
+    double secs;
+    FILE *out;
+
+    if (argc < 4) {
+        fprintf(stderr, "usage: rxloop CHUNK DESC OUT [timing|verify] [THREADS]\n");
+        return 1;
+    }
+    timing = argc > 4 && strcmp(argv[4], "timing") == 0;
+    threads = argc > 5 ? atoi(argv[5]) : 1;
+    if (threads < 1 || threads > 64) { fprintf(stderr, "THREADS: 1..64\n"); return 1; }
+    buf = slurp(argv[1], &nb);
+    desc = slurp(argv[2], &nd);
+    n = (uint32_t)(nd / sizeof(mtcp_gpu_desc));
+    status = calloc(n + 1, 1);
+    ws = calloc((size_t)threads, sizeof(*ws));
+
+    gpu_inner_module = &fake_module;
+    gpu_module_func.load_module();
+    pthread_barrier_init(&g_start, NULL, (unsigned)threads);
+    for (t = 0; t < threads; t++) {                   /* contiguous shards */
+        struct worker *w = &ws[t];
+        const uint32_t lo = (uint32_t)((uint64_t)n * t / threads);
+        const uint32_t hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
+        w->cpu = t;
+        w->timing = timing;
+        w->first = lo;
+        w->status = status + lo;
+        w->fake.buf = buf;
+        w->fake.desc = desc + lo;
+        w->fake.n = hi - lo;
+        if (pthread_create(&w->tid, NULL, worker_main, w) != 0) { perror("pthread_create"); return 1; }
+    }
+    t1 = g_t0;
+    for (t = 0; t < threads; t++) {
+        struct worker *w = &ws[t];
+        pthread_join(w->tid, NULL);
+        rx_packets += w->rx_packets;
+        rx_errors += w->rx_errors;
+        changed += w->changed;
+        hdr_sum += w->hdr_sum;
+        rounds += w->rounds;
+        recv_calls += w->fake.recv_calls;
+        seen += w->seen;
+        if (t == 0 || w->t1.tv_sec > t1.tv_sec ||
+            (w->t1.tv_sec == t1.tv_sec && w->t1.tv_nsec > t1.tv_nsec))
+            t1 = w->t1;
+    }
+    for (uint32_t k = 0; k < n; k++) frame_bytes += desc[k].len;
 
     out = fopen(argv[3], "wb");
-    if (!out || fwrite(status, 1, g_fake.n, out) != g_fake.n) { perror(argv[3]); return 1; }
+    if (!out || fwrite(status, 1, n, out) != n) { perror(argv[3]); return 1; }
     fclose(out);
-    secs = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    secs = (double)(t1.tv_sec - g_t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - g_t0.tv_nsec);
     printf("{\"frames\": %u, \"seen\": %u, \"rounds\": %d, \"inner_bursts\": %d, "
            "\"rx_packets\": %llu, \"rx_errors\": %llu, \"changed\": %llu, "
            "\"ioctl_rx_ip\": %d, \"ioctl_rx_tcp\": %d, \"seconds\": %.6f, "
-           "\"frame_bytes\": %llu, \"timing_mode\": %d, \"hdr_sum\": %llu}\n",
-           g_fake.n, seen, rounds, g_fake.recv_calls, (unsigned long long)rx_packets,
-           (unsigned long long)rx_errors, (unsigned long long)changed, ioctl_ip, ioctl_tcp, secs,
-           (unsigned long long)frame_bytes, timing, (unsigned long long)hdr_sum);
+           "\"frame_bytes\": %llu, \"timing_mode\": %d, \"hdr_sum\": %llu, \"threads\": %d}\n",
+           n, seen, rounds, recv_calls, (unsigned long long)rx_packets,
+           (unsigned long long)rx_errors, (unsigned long long)changed, ws[0].ioctl_ip,
+           ws[0].ioctl_tcp, secs, (unsigned long long)frame_bytes, timing,
+           (unsigned long long)hdr_sum, threads);
     return 0;
 }

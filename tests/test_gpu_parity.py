@@ -77,6 +77,18 @@ def test_rx_golden_host_path(gpu, golden):
     assert not bad, bad
 
 
+def test_rx_golden_host_path_after_reserve(gpu, golden):
+    """mtcp_gpu_reserve (staging + kernels at init), smaller and larger than
+    one call needs: the host path's results are unchanged."""
+    for max_bytes, max_pkts in ((0, 0), (4096, 64), (golden.buf.nbytes, len(golden.desc)),
+                                (1 << 30, 1 << 20)):
+        with gpu.Context(0, rss=True, rss_queues=golden.rss_num_queues) as ctx:
+            ctx.reserve(max_bytes, max_pkts)
+            got = ctx.rx_chunk(golden.buf, golden.desc, 0)
+        bad = compare_results(got, golden)
+        assert not bad, (max_bytes, max_pkts, bad)
+
+
 def test_rx_golden_pointer_burst(gpu, golden):
     """mtcp_gpu_rx_ptrs_dev: a DPDK-style (pointer, len) burst."""
     b = to_dev(golden.buf)

@@ -1,0 +1,70 @@
+"""include/mtcp_gpu_rxq.h on the GPU: frames pushed one by one (as
+gpu_module.c does with the wrapped backend's get_rptr pointers), checked by
+a synchronous flush or by flush_async + wait, served by rxq_get: NULL
+exactly for the checksum failures (ip_in.c:35-36, tcp_in.c:1167-1173), the
+staged frame byte for byte otherwise, and every result record equal to the
+oracle's for the same frame."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from mtcp_amd import RESULT_DTYPE
+
+torch = pytest.importorskip("torch")
+
+V_IP_CSUM_BAD, V_TCP_CSUM_BAD, V_BAD_DESC = 4, 9, 11
+EINVAL = -22
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_rxq_serves_the_oracle_verdicts(golden, mode):
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    from mtcp_amd import gpu
+    from mtcp_amd._lib import lib
+    L = lib()
+    buf, desc = golden.buf, golden.desc
+    want = oracle.rx_chunk(buf, desc, 0)
+    base = buf.ctypes.data
+    agg = 1000                                     # frames per flush
+    with gpu.Context(0) as ctx:
+        q = ctypes.c_void_p()
+        assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, agg, agg * 2048) == 0
+        try:
+            for first in range(0, len(desc), agg):
+                L.mtcp_gpu_rxq_reset(q)
+                part = desc[first:first + agg]
+                for d in part:
+                    assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
+                assert L.mtcp_gpu_rxq_pending(q) == len(part)
+                n_done = ctypes.c_uint32()
+                if mode == "sync":
+                    assert L.mtcp_gpu_rxq_flush(q, ctypes.byref(n_done)) == 0
+                else:
+                    assert L.mtcp_gpu_rxq_flush_async(q) == 0
+                    # in flight: the staging is the GPU's until rxq_wait
+                    assert L.mtcp_gpu_rxq_push(q, base, 64) == EINVAL
+                    assert L.mtcp_gpu_rxq_flush_async(q) == EINVAL
+                    L.mtcp_gpu_rxq_reset(q)                  # refused silently
+                    assert L.mtcp_gpu_rxq_pending(q) == len(part)
+                    assert L.mtcp_gpu_rxq_wait(q, ctypes.byref(n_done)) == 0
+                assert n_done.value == len(part) and L.mtcp_gpu_rxq_pending(q) == 0
+                for i, d in enumerate(part):
+                    k = first + i
+                    ln = ctypes.c_uint16()
+                    res = ctypes.c_void_p()
+                    p = L.mtcp_gpu_rxq_get(q, i, ctypes.byref(ln), ctypes.byref(res))
+                    got = np.frombuffer(ctypes.string_at(res.value, 40), dtype=RESULT_DTYPE)[0]
+                    if want["verdict"][k] != V_BAD_DESC:
+                        assert got.tobytes() == want[k].tobytes(), k
+                    drop = got["verdict"] in (V_IP_CSUM_BAD, V_TCP_CSUM_BAD)
+                    assert (p is None) == drop, k
+                    assert ln.value == d["len"]
+                    if p is not None:
+                        frame = buf[int(d["offset"]):int(d["offset"]) + int(d["len"])]
+                        assert ctypes.string_at(p, int(d["len"])) == frame.tobytes(), k
+        finally:
+            L.mtcp_gpu_rxq_destroy(q)

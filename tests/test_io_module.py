@@ -27,11 +27,12 @@ def build_rxloop() -> str:
     return os.path.join(ROOT, "tests", "c", "rxloop")
 
 
-def run_rxloop(tmp_path):
+def run_rxloop(tmp_path, threads=1, pipeline="1"):
     exe = build_rxloop()
     status = tmp_path / "status.bin"
     p = subprocess.run([exe, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
-                        str(status)], capture_output=True, text=True, timeout=300)
+                        str(status), "verify", str(threads)], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, MTCP_GPU_PIPELINE=pipeline))
     assert p.returncode == 0, p.stderr
     return json.loads(p.stdout.strip().splitlines()[-1]), np.fromfile(status, dtype=np.uint8)
 
@@ -65,9 +66,10 @@ def test_passthrough_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_module_drops_exactly_the_checksum_failures(tmp_path, golden):
+@pytest.mark.parametrize("pipeline", ["1", "0"])
+def test_gpu_module_drops_exactly_the_checksum_failures(tmp_path, golden, pipeline):
     import oracle
-    stats, status = run_rxloop(tmp_path)
+    stats, status = run_rxloop(tmp_path, pipeline=pipeline)
     v = oracle.rx_chunk(golden.buf, golden.desc, 0)["verdict"]
     drop = (v == V_IP_CSUM_BAD) | (v == V_TCP_CSUM_BAD)
     assert stats["seen"] == stats["frames"] == len(golden.desc)
@@ -81,3 +83,21 @@ def test_gpu_module_drops_exactly_the_checksum_failures(tmp_path, golden):
     assert stats["ioctl_rx_ip"] == 0 and stats["ioctl_rx_tcp"] == 0
     # bursts were aggregated: fewer GPU launches than PSIO bursts
     assert stats["rounds"] < stats["inner_bursts"] / 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", ["1", "0"])
+def test_gpu_module_one_context_per_thread(tmp_path, golden, pipeline):
+    """mTCP's share-nothing threads (core.c:1057): four threads, each with its
+    own mtcp_thread_context, gpu_module context, GPU ctx and staging, over
+    contiguous shards of the chunk, drop exactly the single-thread set."""
+    import oracle
+    stats, status = run_rxloop(tmp_path, threads=4, pipeline=pipeline)
+    v = oracle.rx_chunk(golden.buf, golden.desc, 0)["verdict"]
+    drop = (v == V_IP_CSUM_BAD) | (v == V_TCP_CSUM_BAD)
+    assert stats["threads"] == 4
+    assert stats["seen"] == stats["frames"] == len(golden.desc)
+    assert np.array_equal(status == 0, drop)
+    assert (status[~drop] == 1).all() and stats["changed"] == 0
+    assert stats["rx_errors"] == int(drop.sum())
+    assert stats["ioctl_rx_ip"] == 0 and stats["ioctl_rx_tcp"] == 0

@@ -5,8 +5,14 @@
 into the rxq's pinned staging, 64 bursts (4096 frames) go to the GPU per
 launch (H2D, rx kernel, D2H of the records), and get_rptr serves the staged
 frames.  Frames come from the GPU generator (include/mtcp_gpu_pktgen.h),
-copied to host memory first.  Prints one JSON line per frame size.
+copied to host memory first.  Prints one JSON line per frame size and mode,
+then the timing mode with 2, 4 and 8 mTCP threads (one mtcp_thread_context,
+gpu_module context and GPU ctx each, contiguous shards: core.c:1057's
+share-nothing threads sharing one GPU).
   usage: python tools/io_path_bench.py [n_frames]
+         python tools/io_path_bench.py n_frames --dump DIR SIZE   (write the
+             chunk and descriptor files rxloop reads for one frame size, e.g.
+             to run rxloop under rocprofv3)
 """
 import json
 import os
@@ -22,7 +28,7 @@ sys.path.insert(0, ROOT)
 from mtcp_amd import gpu, pktgen  # noqa: E402
 
 
-def run(n, size, seed, tmp, mode):
+def run(n, size, seed, tmp, mode, threads=1, pipeline=True):
     desc, nbytes = pktgen.layout(n, size, 6, seed)
     dev = torch.device("cuda", 0)
     d_buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
@@ -37,29 +43,54 @@ def run(n, size, seed, tmp, mode):
     exe = os.path.join(ROOT, "tests", "c", "rxloop")
     best = None
     for _ in range(3):
-        r = subprocess.run([exe, chunk, dpath, opath] + (["timing"] if mode == "timing" else []),
-                           capture_output=True, text=True, check=True)
+        env = dict(os.environ, MTCP_GPU_PIPELINE="1" if pipeline else "0")
+        r = subprocess.run([exe, chunk, dpath, opath, mode, str(threads)],
+                           capture_output=True, text=True, check=True, env=env)
         st = json.loads(r.stdout.strip().splitlines()[-1])
         if best is None or st["seconds"] < best["seconds"]:
             best = st
     s = best["seconds"]
-    return {"probe": "io_module_path", "mode": mode, "frame_size": size, "frames": n,
+    return {"probe": "io_module_path", "mode": mode, "threads": threads, "pipeline": pipeline,
+            "frame_size": size,
+            "frames": n,
             "bursts_per_launch": 64, "burst": 64, "seconds": s,
             "mpkt_per_s": round(n / s / 1e6, 3), "GBs": round(best["frame_bytes"] / s / 1e9, 3),
             "rx_errors": best["rx_errors"], "changed": best["changed"],
             "ioctl_rx_tcp": best["ioctl_rx_tcp"],
-            "note": "one mTCP thread: copy into pinned staging + H2D + rx kernel + D2H per 4096 "
-                    "frames, get_rptr from staging; mode timing: the first 64 B of each served "
+            "note": "each mTCP thread: copy into pinned staging + one H2D (frames + descriptors) + "
+                    "rx kernel + D2H per 4096 frames, get_rptr from staging; pipelined: aggregate "
+                    "k served while k+1 is on the GPU; mode timing: the first 64 B of each served "
                     "frame read (as ProcessPacket's parse would), mode verify: every served frame "
                     "compared with the original; wall clock of the rx loop, best of 3"}
 
 
+def dump(n, size, seed, out_dir):
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    dev = torch.device("cuda", 0)
+    d_buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+    gpu.pktgen_dev(d_buf, d_desc, n, 6, seed)
+    bdesc = desc.copy()
+    bdesc["offset"] = desc["offset"] << 6
+    os.makedirs(out_dir, exist_ok=True)
+    d_buf.cpu().numpy().tofile(os.path.join(out_dir, "chunk.bin"))
+    bdesc.tofile(os.path.join(out_dir, "desc.bin"))
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
+    if len(sys.argv) > 4 and sys.argv[2] == "--dump":
+        size = sys.argv[4] if sys.argv[4] == "bimodal" else int(sys.argv[4])
+        seeds = {64: 1, 1500: 2, "bimodal": 3}
+        dump(n, size, seeds.get(size, 7), sys.argv[3])
+        return
     with tempfile.TemporaryDirectory() as tmp:
         for size, seed in ((1500, 2), (64, 1), ("bimodal", 3)):
-            for mode in ("timing", "verify"):
-                print(json.dumps(run(n, size, seed, tmp, mode)), flush=True)
+            for mode, pipeline in (("timing", True), ("timing", False), ("verify", True)):
+                print(json.dumps(run(n, size, seed, tmp, mode, 1, pipeline)), flush=True)
+        for size, seed in ((1500, 2), (64, 1)):
+            for threads in (2, 4, 8):
+                print(json.dumps(run(n, size, seed, tmp, "timing", threads)), flush=True)
 
 
 if __name__ == "__main__":

@@ -379,6 +379,9 @@ int main(int argc, char **argv) {
         // variant 0 = what mtcp_gpu.hip dispatches for C3; every other variant's
         // records must equal its records byte for byte
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
+        vs.push_back({"rss_sorted6_fullgrid", rx_kernel<kRxChunk, true, 6>, 1u << 20});
+        vs.push_back({"rss_sorted6_cu4", rx_kernel<kRxChunk, true, 6>, 4});
+        vs.push_back({"rss_sorted6_cu8", rx_kernel<kRxChunk, true, 6>, 8});
         vs.push_back({"ptrs_rss_unrolled_lalign_cu2", rx_kernel<kRxPtrs, true, 3, true>, 2});
         vs.push_back({"ptrs_rss_sorted6_lalign_cu2", rx_kernel<kRxPtrs, true, 6, true>, 2});
         vs.push_back({"rss_rolled_cu2", rx_kernel<kRxChunk, true, 0>, 2});
@@ -395,6 +398,10 @@ int main(int argc, char **argv) {
     } else {
         // variant 0 = what mtcp_gpu.hip dispatches for C2 (C5 adds LALIGN)
         vs.push_back({"unrolled_cu2", rx_kernel<kRxChunk, false, 3>, 2});
+        vs.push_back({"unrolled_fullgrid", rx_kernel<kRxChunk, false, 3>, 1u << 20});
+        vs.push_back({"unrolled_cu4", rx_kernel<kRxChunk, false, 3>, 4});
+        vs.push_back({"unrolled_cu8", rx_kernel<kRxChunk, false, 3>, 8});
+        vs.push_back({"unrolled_lalign_rev_fullgrid", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true>, 1u << 20});
         vs.push_back({"unrolled_lalign_cu2", rx_kernel<kRxChunk, false, 3, true>, 2});
         vs.push_back({"unrolled_lalign_rev_cu2", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true>, 2});
         vs.push_back({"ptrs_unrolled_lalign_cu2", rx_kernel<kRxPtrs, false, 3, true>, 2});
