@@ -335,11 +335,29 @@ int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
     // at stage 0; later stages are used only by calls larger than one stage
     const uint64_t bytes = std::min(max_bytes, kStageBytes);
     const uint32_t pkts = std::min(max_pkts, kStagePkts);
-    const int stages = max_bytes > kStageBytes || max_pkts > kStagePkts ? kStages : 1;
+    const int stages = max_bytes == 0 && max_pkts == 0                  ? 0   // kernels only
+                       : max_bytes > kStageBytes || max_pkts > kStagePkts ? kStages
+                                                                          : 1;
     for (int i = 0; i < stages; ++i) {
         const int rc = stage_reserve(ctx->stage[i], ((bytes + 15) & ~15ull) + 16, std::max(pkts, 1u));
         if (rc != MTCP_GPU_OK) return rc;
     }
+    // a stream sets up its copy queues on its first large copy (7.8 ms
+    // measured): do that here for the stages the host calls use
+    const size_t warm = (size_t)std::min<uint64_t>(ctx->stage[0].buf_cap, 1ull << 20);
+    void *h = nullptr;
+    if (stages && !HIP_OK(hipHostMalloc(&h, warm, hipHostMallocDefault))) return MTCP_GPU_ENOMEM;
+    memset(h, 0, warm);
+    bool ok = true;
+    for (int i = 0; i < stages && ok; ++i) {
+        Stage &st = ctx->stage[i];
+        const size_t w = (size_t)std::min<uint64_t>(warm, st.buf_cap);
+        ok = HIP_OK(hipMemcpyAsync(st.d_buf, h, w, hipMemcpyHostToDevice, st.stream)) &&
+             HIP_OK(hipMemcpyAsync(h, st.d_buf, w, hipMemcpyDeviceToHost, st.stream)) &&
+             HIP_OK(hipStreamSynchronize(st.stream));
+    }
+    if (h) (void)hipHostFree(h);
+    if (!ok) return MTCP_GPU_EIO;
     // the code object loads on the first launch of any of its kernels
     hipFuncAttributes attr;
     if (!HIP_OK(hipFuncGetAttributes(

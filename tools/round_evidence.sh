@@ -24,4 +24,4 @@ bash tools/gpu_steps.sh \
   "v5|200|./tools/rx_variants c5 3" \
   "sp|100|./tools/store_probe" \
   "pc|100|./tools/pcie_probe" \
-  "io|200|python tools/io_path_bench.py 262144"
+  "io|400|python tools/io_path_bench.py 1048576"
