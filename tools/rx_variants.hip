@@ -296,6 +296,45 @@ __global__ __launch_bounds__(256) void ladder(mg::KParams kp) {
 }
 
 
+// The north star's literal shape (BASELINE.json): one wavefront per packet.
+// The wave's 64 lanes stream the frame on the 16 B chunk grid, two loads per
+// lane in flight (2 KiB per wave-instruction pair: a 1500 B frame is one
+// trip), v_sad_u16 halves, a DPP row reduction and a cross-row readlane
+// reduction, then lanes 0..9 store a 40 B record {chunk sum, 0...}: the same
+// records as rx_kernel's ABL 1 (phase 1 alone, chunk sums stored), against
+// which it is compared byte for byte.  PERSIST: waves loop over packets with
+// a capped grid; otherwise one packet per wave and the hardware dispatcher
+// fills the GPU (uncapped grid of n/4 workgroups).
+template <bool PERSIST>
+__global__ __launch_bounds__(256) void wave_per_packet(mg::KParams kp) {
+    using namespace mg;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t step = PERSIST ? gridDim.x * 4 : kp.n;
+    const uint64_t base = (uint64_t)(uintptr_t)kp.buf;
+    for (uint32_t k = wave; k < kp.n; k += step) {
+        const uint64_t raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
+        const uint64_t p = base + ((uint64_t)(uint32_t)raw << kp.off_shift);
+        const uint32_t L = (uint32_t)(raw >> 32) & 0xFFFFu;
+        const uint64_t p16 = p & ~15ull;
+        const uint32_t nch = (uint32_t)((((p + L + 15) & ~15ull) - p16) >> 4);
+        uint32_t acc = 0;
+        for (uint32_t c0 = 0; c0 < nch; c0 += 128) {
+            const uint32_t ca = c0 + lane, cb = c0 + 64 + lane;
+            const v4u xa = gload_nt(p16 + 16ull * (ca < nch ? ca : nch - 1));
+            const v4u xb = gload_nt(p16 + 16ull * (cb < nch ? cb : nch - 1));
+            const uint32_t sa = halves4(xa, 0u), sb = halves4(xb, 0u);
+            acc += (ca < nch ? sa : 0u) + (cb < nch ? sb : 0u);
+        }
+        acc = row_sum(acc);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)acc, 15) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 31) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 47) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 63);
+        if (lane < 10) reinterpret_cast<uint32_t *>(kp.out + k)[lane] = lane == 0 ? tot : 0u;
+    }
+}
+
 struct Variant { const char *name; kfn fn; uint32_t blocks_per_cu; };
 
 static uint64_t mix(uint64_t z) {
@@ -393,6 +432,9 @@ int main(int argc, char **argv) {
         vs.push_back({"abl1_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 1>, 2});
         vs.push_back({"abl2_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 2>, 2});
         vs.push_back({"abl1_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0>, 2});
+        vs.push_back({"wpp_fullgrid", wave_per_packet<false>, 1u << 20});
+        vs.push_back({"wpp_persist_cu2", wave_per_packet<true>, 2});
+        vs.push_back({"wpp_persist_cu8", wave_per_packet<true>, 8});
         vs.push_back({"norss_sorted6_cu2", rx_kernel<kRxChunk, false, 6>, 2});
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
     } else {
@@ -417,6 +459,9 @@ int main(int argc, char **argv) {
         vs.push_back({"abl1_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 1>, 2});
         vs.push_back({"abl2_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 2>, 2});
         vs.push_back({"abl3_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 3>, 2});
+        vs.push_back({"wpp_fullgrid", wave_per_packet<false>, 1u << 20});
+        vs.push_back({"wpp_persist_cu2", wave_per_packet<true>, 2});
+        vs.push_back({"wpp_persist_cu8", wave_per_packet<true>, 8});
         if (strcmp(cfg, "c2") == 0) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
             vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
@@ -439,11 +484,14 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     std::vector<std::vector<float>> ms(vs.size());
+    // the ABL 1 records (chunk sums), which the one-wave-per-packet variants must equal
+    std::vector<mtcp_gpu_result> abl1_rec;
     const int reps = 20;
     for (int r = 0; r < rounds; ++r) {
         for (size_t v = 0; v < vs.size(); ++v) {
             const uint32_t groups = (n + 63) / 64;
-            uint32_t blocks = strstr(vs[v].name, "plain") ? 1u << 20 : (groups + 3) / 4;
+            uint32_t blocks = strstr(vs[v].name, "plain") ? 1u << 20
+                              : strstr(vs[v].name, "wpp") ? (n + 3) / 4 : (groups + 3) / 4;
             if (blocks > cus * vs[v].blocks_per_cu) blocks = cus * vs[v].blocks_per_cu;
             kp.out = v == 0 ? d_ref : d_out;
             CK(hipMemset(kp.out, 0, n * sizeof(mtcp_gpu_result)));
@@ -457,7 +505,19 @@ int main(int argc, char **argv) {
             float t;
             CK(hipEventElapsedTime(&t, a, b));
             ms[v].push_back(t / reps);
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad")) {
+            if (r == 0 && (!strcmp(vs[v].name, "abl1_unrolled_cu2") || !strcmp(vs[v].name, "abl1_rss_sorted6_cu2"))) {
+                abl1_rec.resize(n);
+                CK(hipMemcpy(abl1_rec.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
+            }
+            if (r == 0 && strstr(vs[v].name, "wpp")) {
+                std::vector<mtcp_gpu_result> y(n);
+                CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
+                if (abl1_rec.size() != n || memcmp(abl1_rec.data(), y.data(), n * sizeof(mtcp_gpu_result)) != 0) {
+                    fprintf(stderr, "variant %s differs from the ABL 1 chunk sums\n", vs[v].name);
+                    return 2;
+                }
+            }
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "wpp") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad")) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
