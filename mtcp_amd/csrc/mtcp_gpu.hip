@@ -213,6 +213,10 @@ hipStream_t pick(mtcp_gpu_ctx *ctx, void *stream) {
 }
 
 int stage_reserve(Stage &s, uint64_t bytes, uint32_t pkts) {
+    // growing frees buffers that the stage's previous batch may still use:
+    // drain that batch first rather than rely on hipFree's implicit sync
+    if ((bytes > s.buf_cap || pkts > s.pkt_cap) && s.stream && !HIP_OK(hipStreamSynchronize(s.stream)))
+        return MTCP_GPU_EIO;
     if (bytes > s.buf_cap) {
         if (s.d_buf) (void)hipFree(s.d_buf);
         s.d_buf = nullptr;
