@@ -188,3 +188,34 @@ def test_rss_queue_every_nq_and_endian(gpu):
                     got = run_rx_dev(ctx, buf, desc, 6)
                 assert np.array_equal(got["rss_hash"], want["rss_hash"]), (nq, endian)
                 assert np.array_equal(got["rss_queue"], want["rss_queue"]), (nq, endian)
+
+
+def test_host_pipeline_stage_growth_mid_call(gpu):
+    """Small frames first (three 64 K-descriptor batches of 64 B frames size
+    the stages at ~4 MiB), then 9000 B frames whose batches need 64 MiB: each
+    stage grows while the stages' earlier batches may still be in flight.
+    Every record equals the device path's on the same frames."""
+    seed = 43
+    n_small, n_big = 3 * (1 << 16), 20000
+    lens = np.concatenate([np.full(n_small, 64), np.full(n_big, 9000)]).astype(np.uint16)
+    desc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    slots = (lens.astype(np.int64) + 63) & ~63
+    offs = np.concatenate([[0], np.cumsum(slots)[:-1]])
+    desc["offset"] = (offs >> 6).astype(np.uint32)
+    desc["len"] = lens
+    nbytes = int(slots.sum())
+    n = len(desc)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    d = to_dev(desc)
+    gpu.pktgen_dev(b, d, n, 6, seed)
+    out = dev_results(n)
+    with gpu.Context(0, rss=True, rss_queues=3) as ctx:
+        ctx.rx_chunk_dev(b, d, n, 6, out)
+        torch.cuda.synchronize()
+        dev = out.cpu().numpy().view(RESULT_DTYPE)
+    host = b.cpu().numpy()
+    with gpu.Context(0, rss=True, rss_queues=3) as fresh:   # empty stages: growth happens in this call
+        got = fresh.rx_chunk(host, desc, 6)
+    assert_same(got, dev, "stage growth")
+    idx = np.sort(np.random.default_rng(2).choice(n, size=1000, replace=False))
+    assert_same(got[idx], oracle.rx_chunk(host, desc[idx], 6, oracle.rss_cfg(None, 3, 1)), "sample")
