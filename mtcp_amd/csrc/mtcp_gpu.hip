@@ -150,6 +150,14 @@ void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
                        st, kp);
 }
 
+// Small batches (one io_module aggregate is 4096 frames) give each wave one
+// pass, so phase 1 is latency-bound: the sorted rounds, double-buffered, beat
+// the single-buffered unrolled ones there also for MTU frames (tools/rx_variants
+// RXV_N, 1500 B frames: 4096 -> 13.6 vs 15.0 us, 65536 -> 19.4 vs 22.4 us;
+// 1 M -> 248 vs 243 us, so large batches keep the unrolled rounds).  Jumbo
+// frames keep the unrolled, line-aligned rounds at every size.
+constexpr uint32_t kSortedUpToPkts = 1u << 16;
+
 template <int MODE, bool RSS>
 void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, uint64_t slot) {
     if constexpr (MODE == mg::kRxPtrs) {
@@ -159,7 +167,7 @@ void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, 
         // 245.3, C5-shaped 687.7 vs 685.2 (tools/rx_variants ptrs_*)
         launch_one<MODE, RSS, mg::kSchedSorted, true>(grid, block, st, kp);
     } else {
-        if (slot < kUnrollBelowSlotBytes)
+        if (slot < kUnrollBelowSlotBytes || (kp.n <= kSortedUpToPkts && slot <= kLineAlignAboveSlotBytes))
             launch_one<MODE, RSS, mg::kSchedSorted, false>(grid, block, st, kp);
         else if (slot > kLineAlignAboveSlotBytes)
             launch_one<MODE, RSS, mg::kSchedUnrolled, true>(grid, block, st, kp);

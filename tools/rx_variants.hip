@@ -352,6 +352,7 @@ int main(int argc, char **argv) {
     uint64_t seed = 2;
     if (!strcmp(cfg, "c3")) { bimodal = 1; rss = 1; seed = 3; }
     if (!strcmp(cfg, "c5")) { n = 1u << 19; L = 9000; seed = 5; }
+    if (getenv("RXV_N")) n = (uint32_t)atoi(getenv("RXV_N"));   // e.g. one io_module aggregate (4096)
 
     std::vector<mtcp_gpu_desc> desc(n);
     uint64_t off = 0, frame_bytes = 0;
