@@ -1,6 +1,7 @@
 """Frames at every 4-byte alignment inside a 128 B line, through each phase-1
 schedule the library dispatches (mtcp_gpu.hip launch_sched): size-sorted
-rounds (average slot < 1 KiB), unrolled rounds (<= 1536 B) and unrolled
+rounds (average slot < 1 KiB, or <= 1536 B in batches of at most 64 K
+packets), unrolled rounds (<= 1536 B in larger batches) and unrolled
 rounds with line-aligned trips (> 1536 B, rx_kernel LALIGN, where the first
 trip of a multi-trip frame starts (p16 & 127) / 16 chunks before the frame).
 Multi-trip frames (> 1536 B) appear in all three.  Frames come from the
@@ -57,10 +58,15 @@ def _unaligned_batch(kind, n=1536, seed=11):
     return buf, desc
 
 
-@pytest.mark.parametrize("kind,slot_lo,slot_hi", [("jumbo", 1537, 1 << 30), ("mid", 1024, 1536),
-                                                  ("small", 0, 1023)])
-def test_unaligned_frames_every_schedule(gpu, kind, slot_lo, slot_hi):
-    buf, desc = _unaligned_batch(kind)
+# mtcp_gpu.hip launch_sched: slot > 1536 B -> unrolled + LALIGN; 1024..1536 B
+# -> unrolled above kSortedUpToPkts (64 K) packets, sorted at or below it;
+# < 1 KiB -> sorted.
+@pytest.mark.parametrize("kind,slot_lo,slot_hi,n", [("jumbo", 1537, 1 << 30, 1536),
+                                                    ("mid", 1024, 1536, (1 << 16) + 512),
+                                                    ("mid", 1024, 1536, 1536),
+                                                    ("small", 0, 1023, 1536)])
+def test_unaligned_frames_every_schedule(gpu, kind, slot_lo, slot_hi, n):
+    buf, desc = _unaligned_batch(kind, n)
     padded = buf.nbytes + (-buf.nbytes) % 16
     assert slot_lo <= padded // len(desc) <= slot_hi        # the schedule under test is dispatched
     assert (desc["len"] > 1536).sum() > 50                    # multi-trip frames present
