@@ -9,6 +9,12 @@ generated on the GPU (include/mtcp_gpu_pktgen.h) and stay in HBM; results
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
 
+MTCP_BENCH_DEVICE=d in the environment puts every rank on device d (a
+rehearsal of the N > 1 path on a one-GPU box; the timings then mean
+nothing), and --dump-records DIR writes each rank's result records after the
+timed steps (tests/test_gpu_shard.py compares them with one launch over the
+whole batch).
+
 Multi-GPU: one process per GPU (torch.distributed.run), weak scaling — each
 rank processes its own contiguous shard of one global batch (batch split, no
 collective on the data path; gloo carries only the barrier and the max of the
@@ -22,6 +28,7 @@ frames copied to host memory.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import time
@@ -75,6 +82,13 @@ def parse():
                     help="packets in the CPU sample (default: the whole 1-GPU batch, "
                          "larger than the host L3, so the CPU streams from DRAM like the GPU)")
     ap.add_argument("--pcie", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--pcie-max-bytes", type=int, default=1 << 30,
+                    help="frame bytes per rank in the PCIe-inclusive leg (a prefix of the "
+                         "shard, staged to host memory piece by piece)")
+    ap.add_argument("--per-gpu", type=int, default=None,
+                    help="packets per GPU (default: the config's; tests use smaller batches)")
+    ap.add_argument("--dump-records", default=None,
+                    help="directory: each rank writes its result records there")
     return ap.parse_args()
 
 
@@ -86,6 +100,31 @@ def cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+def host_prefix(d_buf, desc, max_pkts=None, max_bytes=None):
+    """The shard's first frames copied to host memory, in pieces of 256 MiB
+    (no full-shard host copy: at N = 8 every rank stages at once)."""
+    n = len(desc)
+    if max_pkts is not None:
+        n = min(n, max_pkts)
+    ends = (desc["offset"][:n].astype(np.int64) << 6) + ((desc["len"][:n].astype(np.int64) + 63) & ~63)
+    if max_bytes is not None:
+        n = max(1, int(np.searchsorted(ends, max_bytes, side="right")))
+    end = int(ends[n - 1])
+    host = np.empty(end, np.uint8)
+    step = 256 << 20
+    for o in range(0, end, step):
+        host[o:o + step] = d_buf[o:min(o + step, end)].cpu().numpy()
+    return host, desc[:n]
+
+
+def lib_sha256() -> str:
+    """Identity of the product library whose kernels this run measures: the
+    committed PMC traffic figure (profiles/traffic_*.json) counts only when it
+    was collected on the same build."""
+    from mtcp_amd import _lib
+    return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
 
 
 def cpu_share() -> int:
@@ -160,9 +199,10 @@ def pcie_inclusive(ctx, host_buf, desc, nbytes, world):
         total_bytes, total_pkts = int(tb[0]), int(tb[1])
     return {"value": round(total_bytes / best / 1e9, 3), "unit": "GB/s",
             "gpkt_per_s": round(total_pkts / best / 1e9, 5), "n_gpus": world,
+            "packets_per_rank": len(desc),
             "note": "pinned host chunk in, host results out; H2D + kernel + D2H overlapped "
-                    "on 3 streams, 64 MiB stages; all ranks at once, wall clock max over "
-                    "ranks, best of 3"}
+                    "on 3 streams, 64 MiB stages; each rank its shard's first frames (at most "
+                    "--pcie-max-bytes), all ranks at once, wall clock max over ranks, best of 3"}
 
 
 def _timed(step, steps, warmup, stream):
@@ -308,12 +348,14 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    torch.cuda.set_device(local_rank)
+    device = int(os.environ.get("MTCP_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(device)
     from mtcp_amd import gpu   # loads libmtcp_gpu.so (raises if not built)
 
-    n_total = cfg["per_gpu"] * world
+    per_gpu = args.per_gpu or cfg["per_gpu"]
+    n_total = per_gpu * world
     sh = shard.make_shard(n_total, cfg["size"], rank, world, cfg["seed"])
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", device)
     # a dedicated (non-null) stream: the kernel and the timing events share it
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
@@ -323,7 +365,7 @@ def main():
     gpu.pktgen_dev(d_buf, d_desc, sh.count, 6, cfg["seed"], sh.first_index, stream=stream)
     frame_bytes = int(sh.desc["len"].astype(np.int64).sum())
 
-    ctx = gpu.Context(local_rank, rss=cfg["rss"], rss_queues=8, rss_endian=True)
+    ctx = gpu.Context(device, rss=cfg["rss"], rss_queues=8, rss_endian=True)
     step = lambda: ctx.rx_chunk_dev(d_buf, d_desc, sh.count, 6, d_out, stream=stream)
 
     for _ in range(args.warmup):
@@ -366,55 +408,74 @@ def main():
         kern_ms_max = kern_ms
 
     # verdict summary of the last step (sanity: corruption rate ~1/1024 + 1/4096)
-    res = d_out.view(-1, 40)[:, 36].cpu().numpy()
+    recs = d_out.view(-1, 40)
+    res = recs[:, 36].cpu().numpy()
     ok_frac = float((res == 0).mean())
+    # TCP payload bytes (payload_len of the records, tcp_in.c:1144): the
+    # metric's "payload GB/s" without the 54+ B of headers per frame
+    payload = int(recs[:, 32:34].contiguous().view(torch.int16).to(torch.int64).bitwise_and(0xFFFF).sum())
+    if args.dump_records:
+        os.makedirs(args.dump_records, exist_ok=True)
+        d_out.cpu().numpy().tofile(os.path.join(args.dump_records, f"records_rank{rank}.bin"))
+        json.dump({"rank": rank, "world": world, "first_index": sh.first_index, "count": sh.count},
+                  open(os.path.join(args.dump_records, f"shard_rank{rank}.json"), "w"))
 
-    total_bytes = frame_bytes * world if cfg["size"] != "bimodal" else None
     if world > 1:
-        tb = torch.tensor([frame_bytes, sh.count], dtype=torch.int64)
+        tb = torch.tensor([frame_bytes, sh.count, payload], dtype=torch.int64)
         dist.all_reduce(tb)
-        total_bytes, total_pkts = int(tb[0]), int(tb[1])
+        total_bytes, total_pkts, total_payload = int(tb[0]), int(tb[1]), int(tb[2])
     else:
-        total_bytes, total_pkts = frame_bytes, sh.count
+        total_bytes, total_pkts, total_payload = frame_bytes, sh.count, payload
     ms_per_step = elapsed / args.steps * 1e3
     gbs = total_bytes * args.steps / elapsed / 1e9
     gpps = total_pkts * args.steps / elapsed / 1e9
+    payload_gbs = total_payload * args.steps / elapsed / 1e9
 
     extra = {}
     want_cpu = rank == 0 and world == 1 and args.cpu_baseline in ("on", "auto")
     want_pcie = args.pcie in ("on", "auto")     # every rank: a collective step when N > 1
-    if want_cpu or want_pcie:
-        host = d_buf.cpu().numpy()
-        if want_cpu:
-            try:
-                extra["cpu_baseline"] = cpu_baseline(host, sh.desc, cfg, args.cpu_sample)
-            except Exception as exc:   # report, never fake
-                extra["cpu_baseline"] = {"value": None, "error": repr(exc)}
-        if want_pcie:
-            extra["pcie_inclusive"] = pcie_inclusive(ctx, host, sh.desc, frame_bytes, world)
+    if want_cpu:
+        host, hdesc = host_prefix(d_buf, sh.desc, max_pkts=args.cpu_sample)
+        try:
+            extra["cpu_baseline"] = cpu_baseline(host, hdesc, cfg, args.cpu_sample)
+        except Exception as exc:   # report, never fake
+            extra["cpu_baseline"] = {"value": None, "error": repr(exc)}
+        del host
+    if want_pcie:
+        host, hdesc = host_prefix(d_buf, sh.desc, max_bytes=args.pcie_max_bytes)
+        extra["pcie_inclusive"] = pcie_inclusive(ctx, host, hdesc,
+                                                 int(hdesc["len"].astype(np.int64).sum()), world)
         del host
     ctx.close()
 
     if rank == 0:
-        achieved = frame_bytes / (kern_ms / 1e3) / 1e9
-        traffic = None
+        # per-GPU roofline of the slowest rank's launches (N > 1: the max
+        # over ranks of the event-timed average launch)
+        achieved = frame_bytes / (kern_ms_max / 1e3) / 1e9
+        traffic, traffic_note = None, "no PMC profile for this config"
         tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                              f"traffic_{args.config}.json")
         if os.path.exists(tpath):
-            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+            tj = json.load(open(tpath))
+            if tj.get("lib_sha256") == lib_sha256():
+                traffic = tj.get("hbm_bytes_per_launch")
+                traffic_note = f"rocprofv3 PMC of this build ({os.path.relpath(tpath)})"
+            else:
+                traffic_note = (f"stale: {os.path.relpath(tpath)} was collected on another build "
+                                f"({tj.get('hbm_bytes_per_launch')} B per launch there)")
         line = {
             "metric": METRIC, "value": round(gbs, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (GPU splitmix64 frames, include/mtcp_gpu_pktgen.h)",
-            "gpkt_per_s": round(gpps, 4),
-            "config": {"workload": args.config + ": " + cfg["desc"], "packets_per_gpu": cfg["per_gpu"],
+            "gpkt_per_s": round(gpps, 4), "payload_gbs": round(payload_gbs, 2),
+            "config": {"workload": args.config + ": " + cfg["desc"], "packets_per_gpu": per_gpu,
                        "packets_total": total_pkts, "frame_bytes_total": total_bytes,
                        "rss": cfg["rss"], "parallelism": f"batch split x{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "kernel": "mg::rx_kernel", "avg_launch_ms": round(kern_ms, 5),
+                         "traffic": traffic, "traffic_source": traffic_note,
+                         "kernel": "mg::rx_kernel", "avg_launch_ms": round(kern_ms_max, 5),
                          "algorithmic_bytes_per_launch": frame_bytes},
             "tcp_ok_fraction": round(ok_frac, 5),
         }

@@ -28,6 +28,16 @@
  *       the DISABLE_HWCSUM checksum fills of the tx path:
  *       iph->check = ip_fast_csum(iph, iph->ihl)   (mtcp/src/ip_out.c:94,164)
  *       tcph->check = TCPCalcChecksum(...)          (mtcp/src/tcp_out.c:211,329)
+ *   mtcp_gpu_tx_fill_ptrs / _tx_fill_ptrs_dev
+ *       the same fills for a DPDK-style burst of frame pointers, the batch
+ *       send_pkts hands to the NIC (wmbufs[ifidx].m_table,
+ *       mtcp/src/dpdk_module.c:282-338, filled by get_wptr :341-370); what a
+ *       NIC does after dev_ioctl(PKT_TX_TCPIP_CSUM[_PEEK]) answered 0
+ *       (ip_out.c:147-161, tcp_out.c:320-324).
+ *   mtcp_gpu_rx_chunk_flow_dev / _rx_ptrs_flow_dev
+ *       rx as above plus HashFlow (mtcp/src/tcp_stream.c:56-90) of every
+ *       TCP_OK packet's flow-table key in the same pass (no second launch
+ *       over the records).
  *   mtcp_gpu_flow_hash / _flow_hash_dev
  *       HashFlow (mtcp/src/tcp_stream.c:56-90) of the flow-table lookup key
  *       (mtcp/src/tcp_in.c:1180-1186), the step after the checksums.
@@ -90,9 +100,10 @@ extern "C" {
  * (io_engine/include/ps.h:181-185), so a ps_chunk's info[] array can be
  * passed as is with off_shift = 0.  With off_shift = 6 the offset counts 64 B
  * units (PSIO aligns packets to 64 B, io_engine/lib/pslib.c:146), which
- * reaches 256 GiB chunks.  Byte offset = offset << off_shift; it must be a
- * multiple of 4 and offset + len must lie inside the chunk, otherwise the
- * packet gets MTCP_GPU_V_BAD_DESC and is not read.
+ * reaches 256 GiB chunks.  Byte offset = offset << off_shift; it must be
+ * even (2-byte aligned frame starts, e.g. NET_IP_ALIGN buffers, are fine)
+ * and offset + len must lie inside the chunk, otherwise the packet gets
+ * MTCP_GPU_V_BAD_DESC and is not read.
  * len = frame length as get_rptr's *len (Ethernet header through the end of
  * the frame, CRC stripped; mtcp/src/dpdk_module.c:467).
  */
@@ -206,12 +217,28 @@ int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len
 /*
  * Device-resident rx over a pointer burst.  d_pkts[i] is a device-accessible
  * address (device memory, or host memory registered with
- * mtcp_gpu_host_register: the kernel then reads it over PCIe, zero copy),
- * 4-byte aligned; d_lens[i] its frame length.
+ * mtcp_gpu_host_register: the kernel then reads it over PCIe, zero copy) at
+ * any even address (a NULL or odd pointer gives MTCP_GPU_V_BAD_DESC);
+ * d_lens[i] its frame length.
  */
 int mtcp_gpu_rx_ptrs_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts,
                          const uint16_t *d_lens, uint32_t n,
                          mtcp_gpu_result *d_out, void *stream);
+
+/*
+ * The two device-resident rx calls with the flow-table step fused in:
+ * d_bins[i] = the HashFlow bin of packet i (as mtcp_gpu_flow_hash_dev would
+ * give for d_out[i]: MTCP_GPU_FLOW_NONE unless TCP_OK), computed in the same
+ * kernel from the record it writes.  d_bins may be NULL (then exactly the
+ * calls above).
+ */
+int mtcp_gpu_rx_chunk_flow_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
+                               const mtcp_gpu_desc *d_desc, uint32_t n,
+                               uint32_t off_shift, mtcp_gpu_result *d_out,
+                               uint32_t *d_bins, void *stream);
+int mtcp_gpu_rx_ptrs_flow_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts,
+                              const uint16_t *d_lens, uint32_t n,
+                              mtcp_gpu_result *d_out, uint32_t *d_bins, void *stream);
 
 /*
  * Host-memory rx (the drop-in for the rx loop): chunk and descriptors in host
@@ -245,6 +272,20 @@ int mtcp_gpu_tx_fill_dev(mtcp_gpu_ctx *ctx, void *d_buf, uint64_t buf_len,
 int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len,
                      const mtcp_gpu_desc *desc, uint32_t n, uint32_t off_shift,
                      uint32_t *n_filled);
+
+/*
+ * tx checksum fill of a pointer burst, same rule as mtcp_gpu_tx_fill.
+ *   _dev: d_pkts[i] device-accessible (device memory or registered host
+ *         memory, written in place over PCIe), asynchronous on `stream`.
+ *   host: pkts[i] in host memory; the frames are staged to the GPU, the
+ *         check values come back, and only the two check fields of each
+ *         filled frame are written (by the calling thread); synchronous.
+ *         *n_filled (may be NULL) receives the number of frames filled.
+ */
+int mtcp_gpu_tx_fill_ptrs_dev(mtcp_gpu_ctx *ctx, uint8_t *const *d_pkts,
+                              const uint16_t *d_lens, uint32_t n, void *stream);
+int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_t *lens,
+                          uint32_t n, uint32_t *n_filled);
 
 /* ---- flow-table hash (HashFlow) --------------------------------------- */
 #define MTCP_GPU_NUM_BINS_FLOWS  131072u      /* mtcp/src/include/fhash.h:7 */

@@ -26,23 +26,6 @@ constexpr uint32_t kPorts = MTCP_GPU_MAX_PORT - MTCP_GPU_MIN_PORT;   // 64511
 constexpr int kPoolPerThread = 16;                                   // candidates per lane
 constexpr int kPoolTile = kBlock * kPoolPerThread;                   // per workgroup
 
-// Jenkins one-at-a-time over the 12 key bytes, each read as a signed char
-// (tcp_stream.c:77-87 `char *key`; x86 char is signed).  The bytes of w are
-// key bytes 4q..4q+3 in memory order.
-__device__ __forceinline__ uint32_t hash_flow(const uint32_t (&w)[3]) {
-    uint32_t h = 0;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-        h += (uint32_t)(int32_t)(int8_t)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-        h += h << 10;
-        h ^= h >> 6;
-    }
-    h += h << 3;
-    h ^= h >> 11;
-    h += h << 15;
-    return h & (MTCP_GPU_NUM_BINS_FLOWS - 1);
-}
-
 // One lane per result record: saddr @0, daddr @4, sport|dport @8, verdict @36.
 __global__ __launch_bounds__(kBlock) void flow_hash_kernel(const mtcp_gpu_result *__restrict__ res,
                                                            uint32_t n, uint32_t *__restrict__ bins) {
@@ -50,11 +33,7 @@ __global__ __launch_bounds__(kBlock) void flow_hash_kernel(const mtcp_gpu_result
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         const uint32_t *r = reinterpret_cast<const uint32_t *>(res + i);
         const uint32_t saddr = r[0], daddr = r[1], ports = r[2];
-        const uint32_t verdict = r[9] & 0xFFu;
-        // tcp_in.c:1180-1183: {saddr = iph->daddr, daddr = iph->saddr,
-        //                      sport = tcph->dest, dport = tcph->source}
-        const uint32_t w[3] = {daddr, saddr, (ports >> 16) | (ports << 16)};
-        bins[i] = verdict == MTCP_GPU_V_TCP_OK ? hash_flow(w) : MTCP_GPU_FLOW_NONE;
+        bins[i] = flow_bin(saddr, daddr, ports, r[9] & 0xFFu);   // rx_kernels.hpp
     }
 }
 
@@ -71,14 +50,6 @@ __device__ __forceinline__ uint32_t toeplitz96(const uint32_t *tab, uint32_t sip
         h ^= tab[((16 + t) << 4) | ((ports >> (28 - 4 * t)) & 15u)];
     }
     return h;
-}
-
-// mtcp/src/rss.c:90-103: masked = hash & 0x7F, endian fix off[m & 3] =
-// {3, 1, -1, -3} (i.e. m ^ 3), queue = masked % num_queues.
-__device__ __forceinline__ uint32_t rss_queue(uint32_t h, uint32_t nq, uint32_t endian) {
-    uint32_t m = h & 0x7Fu;
-    if (endian) m ^= 3u;
-    return m % nq;
 }
 
 struct PoolParams {
@@ -112,7 +83,7 @@ __global__ __launch_bounds__(kBlock) void rss_queue_map_kernel(PoolParams pp,
                 const uint32_t port = MTCP_GPU_MIN_PORT + (uint32_t)(g - (uint64_t)i * kPorts);
                 const uint32_t h = toeplitz96(tab, pp.daddr_h, pp.saddr_base_h + i,
                                               (pp.dport_h << 16) | port);
-                word |= rss_queue(h, pp.nq, pp.endian) << (8 * b);
+                word |= rss_core(h, pp.nq, pp.endian) << (8 * b);
             }
         }
         if (4 * q + 3 < pp.total) {

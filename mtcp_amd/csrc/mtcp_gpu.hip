@@ -18,6 +18,7 @@
 #include "flow_kernels.hpp"
 #include "host_copy.hpp"
 #include "rx_kernels.hpp"
+#include "rx_wave.hpp"
 
 namespace {
 
@@ -42,6 +43,8 @@ struct mtcp_gpu_ctx {
     uint32_t flags = 0;
     uint32_t rss_nq = 1;
     uint32_t rss_endian = 0;
+    uint32_t rss_key_w[4] = {0, 0, 0, 0};        // key bytes 0..15, big-endian words
+    uint32_t wave_upto = 0;                      // rx_wave_kernel for batches of <= this many
     hipStream_t stream = nullptr;
     uint32_t *d_rss_tables = nullptr;
     uint32_t *d_count = nullptr;
@@ -159,7 +162,8 @@ void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
 constexpr uint32_t kSortedUpToPkts = 1u << 16;
 
 template <int MODE, bool RSS>
-void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, uint64_t slot) {
+void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, uint64_t slot,
+                  uint32_t batch_n) {
     if constexpr (MODE == mg::kRxPtrs) {
         // pointer bursts carry no size hint the host can see (the lengths are
         // in device memory): the size-sorted rounds are the robust choice —
@@ -167,7 +171,9 @@ void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, 
         // 245.3, C5-shaped 687.7 vs 685.2 (tools/rx_variants ptrs_*)
         launch_one<MODE, RSS, mg::kSchedSorted, true>(grid, block, st, kp);
     } else {
-        if (slot < kUnrollBelowSlotBytes || (kp.n <= kSortedUpToPkts && slot <= kLineAlignAboveSlotBytes))
+        // the schedule is chosen once per batch (batch_n: the whole batch,
+        // not this launch's share of it)
+        if (slot < kUnrollBelowSlotBytes || (batch_n <= kSortedUpToPkts && slot <= kLineAlignAboveSlotBytes))
             launch_one<MODE, RSS, mg::kSchedSorted, false>(grid, block, st, kp);
         else if (slot > kLineAlignAboveSlotBytes)
             launch_one<MODE, RSS, mg::kSchedUnrolled, true>(grid, block, st, kp);
@@ -183,11 +189,32 @@ void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, 
 // cut into launches of at most grid x 4 waves x 64 x kHeldPasses packets.
 constexpr uint32_t kHeldPasses = 8;
 
+// One wavefront per packet (rx_wave.hpp) for small batches: rx_kernel gives
+// a wave 64 packets, so a batch of n packets runs on n/64 waves and its
+// phase 1 is a chain of round trips; the wave kernel puts n waves in flight.
+// Measured crossover: see DESIGN.md §4 (MTCP_GPU_WAVE_UPTO overrides it at
+// context open, for A/B runs and the parity tests of both schedules).
+constexpr uint32_t kWaveUpToPkts = 1u << 15;
+
+template <int MODE, bool RSS>
+void launch_wave(uint32_t n, hipStream_t st, const mg::KParams &kp) {
+    hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS>), dim3((n + mg::kWavesPerBlock - 1) / mg::kWavesPerBlock),
+                       dim3(mg::kBlock), 0, st, kp);
+}
+
 template <int MODE>
 int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     if (kp.n == 0) return MTCP_GPU_OK;
+    const bool rss = !mg::is_tx(MODE) && (ctx->flags & MTCP_GPU_F_RSS);
+    if (MODE == mg::kTxPtrs || kp.tx_report || kp.n <= ctx->wave_upto) {
+        if (rss)
+            launch_wave<MODE, true>(kp.n, st, kp);
+        else
+            launch_wave<MODE, false>(kp.n, st, kp);
+        return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
+    }
+    if constexpr (MODE != mg::kTxPtrs) {
     const dim3 grid(grid_for(ctx, kp.n)), block(mg::kBlock);
-    const bool rss = MODE != mg::kTxChunk && (ctx->flags & MTCP_GPU_F_RSS);
     const uint64_t slot = kp.n ? kp.buf_len / kp.n : 0;       // the whole batch's average slot
     const uint32_t cap = grid.x * mg::kWavesPerBlock * mg::kWave * kHeldPasses;
     for (uint32_t first = 0; first < kp.n; first += cap) {
@@ -200,10 +227,12 @@ int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
             sub.desc = kp.desc + first;
         }
         if (MODE != mg::kTxChunk) sub.out = kp.out + first;
+        if (kp.bins) sub.bins = kp.bins + first;
         if (rss)
-            launch_sched<MODE, true>(grid, block, st, sub, slot);
+            launch_sched<MODE, true>(grid, block, st, sub, slot, kp.n);
         else
-            launch_sched<MODE, false>(grid, block, st, sub, slot);
+            launch_sched<MODE, false>(grid, block, st, sub, slot, kp.n);
+    }
     }
     return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
@@ -213,6 +242,7 @@ mg::KParams base_params(mtcp_gpu_ctx *ctx) {
     kp.rss_tables = ctx->d_rss_tables;
     kp.rss_nq = ctx->rss_nq;
     kp.rss_endian = ctx->rss_endian;
+    for (int i = 0; i < 4; ++i) kp.rss_key[i] = ctx->rss_key_w[i];
     return kp;
 }
 
@@ -300,7 +330,13 @@ int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rs
         ctx->num_cu = prop.multiProcessorCount;
 
     uint32_t tables[mg::kRssTableWords];
-    build_rss_tables(rss_key ? rss_key : key05, tables);
+    const uint8_t *key = rss_key ? rss_key : key05;
+    build_rss_tables(key, tables);
+    for (int i = 0; i < 4; ++i)
+        ctx->rss_key_w[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) |
+                            ((uint32_t)key[4 * i + 2] << 8) | (uint32_t)key[4 * i + 3];
+    ctx->wave_upto = kWaveUpToPkts;
+    if (const char *e = getenv("MTCP_GPU_WAVE_UPTO")) ctx->wave_upto = (uint32_t)strtoul(e, nullptr, 10);
     int rc = MTCP_GPU_OK;
     if (!HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) ||
         !HIP_OK(hipMalloc(&ctx->d_rss_tables, sizeof(tables))) ||
@@ -356,12 +392,12 @@ int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
     }
     // a stream sets up its copy queues on its first large copy (7.8 ms
     // measured): do that here for the stages the host calls use
-    const size_t warm = (size_t)std::min<uint64_t>(ctx->stage[0].buf_cap, 1ull << 20);
+    const size_t warm = stages ? (size_t)std::min<uint64_t>(ctx->stage[0].buf_cap, 1ull << 20) : 0;
     void *h = nullptr;
-    if (stages && !HIP_OK(hipHostMalloc(&h, warm, hipHostMallocDefault))) return MTCP_GPU_ENOMEM;
-    memset(h, 0, warm);
+    if (warm && !HIP_OK(hipHostMalloc(&h, warm, hipHostMallocDefault))) return MTCP_GPU_ENOMEM;
+    if (h) memset(h, 0, warm);
     bool ok = true;
-    for (int i = 0; i < stages && ok; ++i) {
+    for (int i = 0; i < stages && ok && h; ++i) {
         Stage &st = ctx->stage[i];
         const size_t w = (size_t)std::min<uint64_t>(warm, st.buf_cap);
         ok = HIP_OK(hipMemcpyAsync(st.d_buf, h, w, hipMemcpyHostToDevice, st.stream)) &&
@@ -402,11 +438,12 @@ int mtcp_gpu_sync(mtcp_gpu_ctx *ctx) {
     return HIP_OK(hipStreamSynchronize(ctx->stream)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
 
-int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
-                          const mtcp_gpu_desc *d_desc, uint32_t n, uint32_t off_shift,
-                          mtcp_gpu_result *d_out, void *stream) {
+int mtcp_gpu_rx_chunk_flow_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
+                               const mtcp_gpu_desc *d_desc, uint32_t n, uint32_t off_shift,
+                               mtcp_gpu_result *d_out, uint32_t *d_bins, void *stream) {
     if (!ctx || (n && (!d_buf || !d_desc || !d_out)) || off_shift > 16 || (buf_len & 15) ||
-        ((uintptr_t)d_buf & 15) || ((uintptr_t)d_out & 7) || ((uintptr_t)d_desc & 7))
+        ((uintptr_t)d_buf & 15) || ((uintptr_t)d_out & 7) || ((uintptr_t)d_desc & 7) ||
+        ((uintptr_t)d_bins & 3))
         return MTCP_GPU_EINVAL;
     DeviceGuard dg(ctx->device);
     mg::KParams kp = base_params(ctx);
@@ -416,12 +453,20 @@ int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len
     kp.n = n;
     kp.off_shift = off_shift;
     kp.out = d_out;
+    kp.bins = d_bins;
     return launch<mg::kRxChunk>(ctx, kp, pick(ctx, stream));
 }
 
-int mtcp_gpu_rx_ptrs_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts, const uint16_t *d_lens,
-                         uint32_t n, mtcp_gpu_result *d_out, void *stream) {
-    if (!ctx || (n && (!d_pkts || !d_lens || !d_out)) || ((uintptr_t)d_out & 7))
+int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
+                          const mtcp_gpu_desc *d_desc, uint32_t n, uint32_t off_shift,
+                          mtcp_gpu_result *d_out, void *stream) {
+    return mtcp_gpu_rx_chunk_flow_dev(ctx, d_buf, buf_len, d_desc, n, off_shift, d_out, nullptr, stream);
+}
+
+int mtcp_gpu_rx_ptrs_flow_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts, const uint16_t *d_lens,
+                              uint32_t n, mtcp_gpu_result *d_out, uint32_t *d_bins, void *stream) {
+    if (!ctx || (n && (!d_pkts || !d_lens || !d_out)) || ((uintptr_t)d_out & 7) ||
+        ((uintptr_t)d_bins & 3))
         return MTCP_GPU_EINVAL;
     DeviceGuard dg(ctx->device);
     mg::KParams kp = base_params(ctx);
@@ -429,7 +474,24 @@ int mtcp_gpu_rx_ptrs_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts, const 
     kp.lens = d_lens;
     kp.n = n;
     kp.out = d_out;
+    kp.bins = d_bins;
     return launch<mg::kRxPtrs>(ctx, kp, pick(ctx, stream));
+}
+
+int mtcp_gpu_rx_ptrs_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts, const uint16_t *d_lens,
+                         uint32_t n, mtcp_gpu_result *d_out, void *stream) {
+    return mtcp_gpu_rx_ptrs_flow_dev(ctx, d_pkts, d_lens, n, d_out, nullptr, stream);
+}
+
+int mtcp_gpu_tx_fill_ptrs_dev(mtcp_gpu_ctx *ctx, uint8_t *const *d_pkts, const uint16_t *d_lens,
+                              uint32_t n, void *stream) {
+    if (!ctx || (n && (!d_pkts || !d_lens))) return MTCP_GPU_EINVAL;
+    DeviceGuard dg(ctx->device);
+    mg::KParams kp = base_params(ctx);
+    kp.ptrs = reinterpret_cast<const uint8_t *const *>(d_pkts);
+    kp.lens = d_lens;
+    kp.n = n;
+    return launch<mg::kTxPtrs>(ctx, kp, pick(ctx, stream));
 }
 
 int mtcp_gpu_tx_fill_dev(mtcp_gpu_ctx *ctx, void *d_buf, uint64_t buf_len,
@@ -530,12 +592,14 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
     return rc;
 }
 
-int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *lens,
-                     uint32_t n, mtcp_gpu_result *out) {
-    if (!ctx || (n && (!pkts || !lens || !out))) return MTCP_GPU_EINVAL;
-    if (n == 0) return MTCP_GPU_OK;
-    DeviceGuard dg(ctx->device);
-    // gather into a pinned PSIO-style chunk (64 B aligned slots, pslib.c:146)
+}  // extern "C"
+
+namespace {
+
+// Gather a pointer burst into the context's pinned PSIO-style chunk (64 B
+// aligned slots, pslib.c:146) with its descriptors; *total = chunk bytes.
+int gather_burst(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *lens, uint32_t n,
+                 uint64_t *total_out) {
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) total += ((uint64_t)lens[i] + 63) & ~63ull;
     if (total > ctx->h_gather_cap) {
@@ -565,7 +629,71 @@ int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16
         off += ((uint64_t)lens[i] + 63) & ~63ull;
     }
     stage_fence();
+    *total_out = total;
+    return MTCP_GPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *lens,
+                     uint32_t n, mtcp_gpu_result *out) {
+    if (!ctx || (n && (!pkts || !lens || !out))) return MTCP_GPU_EINVAL;
+    if (n == 0) return MTCP_GPU_OK;
+    DeviceGuard dg(ctx->device);
+    uint64_t total = 0;
+    const int rc = gather_burst(ctx, pkts, lens, n, &total);
+    if (rc != MTCP_GPU_OK) return rc;
     return mtcp_gpu_rx_chunk(ctx, ctx->h_gather, total, ctx->h_gather_desc, n, 6, out);
+}
+
+// tx fill of a host pointer burst (a DPDK wmbufs[].m_table, dpdk_module.c:341-370):
+// the frames are gathered into pinned staging and checked on the GPU, which
+// reports {checks, T} per frame (rx_wave_kernel report mode); only the two
+// check fields are written back into the caller's frames, here on the host.
+int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_t *lens, uint32_t n,
+                          uint32_t *n_filled) {
+    if (!ctx || (n && (!pkts || !lens))) return MTCP_GPU_EINVAL;
+    if (n_filled) *n_filled = 0;
+    if (n == 0) return MTCP_GPU_OK;
+    DeviceGuard dg(ctx->device);
+    uint64_t total = 0;
+    int rc = gather_burst(ctx, pkts, lens, n, &total);
+    if (rc != MTCP_GPU_OK) return rc;
+    Stage &s = ctx->stage[0];
+    rc = stage_reserve(s, ((total + 15) & ~15ull) + 16, n);
+    if (rc != MTCP_GPU_OK) return rc;
+    uint2 *report = reinterpret_cast<uint2 *>(ctx->h_gather_desc);    // reused once the H2D is done
+    static_assert(sizeof(uint2) == sizeof(mtcp_gpu_desc), "report reuses the descriptor staging");
+    if (!HIP_OK(hipMemcpyAsync(s.d_buf, ctx->h_gather, total, hipMemcpyHostToDevice, s.stream)) ||
+        !HIP_OK(hipMemcpyAsync(s.d_desc, ctx->h_gather_desc, (size_t)n * sizeof(mtcp_gpu_desc),
+                               hipMemcpyHostToDevice, s.stream)))
+        rc = MTCP_GPU_EIO;
+    mg::KParams kp = base_params(ctx);
+    kp.buf = s.d_buf;
+    kp.buf_len = total;
+    kp.desc = s.d_desc;
+    kp.n = n;
+    kp.off_shift = 6;
+    kp.tx_report = reinterpret_cast<uint2 *>(s.d_out);                // n x 8 B <= n x 40 B
+    if (rc == MTCP_GPU_OK) rc = launch<mg::kTxChunk>(ctx, kp, s.stream);
+    if (rc == MTCP_GPU_OK && !HIP_OK(hipMemcpyAsync(report, s.d_out, (size_t)n * sizeof(uint2),
+                                                    hipMemcpyDeviceToHost, s.stream)))
+        rc = MTCP_GPU_EIO;
+    if (!HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK) rc = MTCP_GPU_EIO;
+    if (rc != MTCP_GPU_OK) return rc;
+    uint32_t cnt = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t T = report[i].y;
+        if (!T) continue;
+        const uint16_t ipc = (uint16_t)report[i].x, tcpc = (uint16_t)(report[i].x >> 16);
+        memcpy(pkts[i] + 24, &ipc, 2);                                 // iph->check   (ip_out.c:164)
+        memcpy(pkts[i] + T + 16, &tcpc, 2);                            // tcph->check  (tcp_out.c:329)
+        ++cnt;
+    }
+    if (n_filled) *n_filled = cnt;
+    return MTCP_GPU_OK;
 }
 
 int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mtcp_gpu_desc *desc,
@@ -578,12 +706,14 @@ int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mt
     const uint64_t cap = (buf_len + 15) & ~15ull;
     int rc = stage_reserve(s, cap + 16, n);
     if (rc != MTCP_GPU_OK) return rc;
+    // an enqueue that fails still drains the stream below: an H2D already
+    // queued may be reading the caller's buf
     if (!HIP_OK(hipMemsetAsync(s.d_buf + (buf_len & ~15ull), 0, 16, s.stream)) ||
         !HIP_OK(hipMemcpyAsync(s.d_buf, buf, buf_len, hipMemcpyHostToDevice, s.stream)) ||
         !HIP_OK(hipMemcpyAsync(s.d_desc, desc, (size_t)n * sizeof(mtcp_gpu_desc),
                                hipMemcpyHostToDevice, s.stream)) ||
         !HIP_OK(hipMemsetAsync(ctx->d_count, 0, sizeof(uint32_t), s.stream)))
-        return MTCP_GPU_EIO;
+        rc = MTCP_GPU_EIO;
     mg::KParams kp = base_params(ctx);
     kp.buf = s.d_buf;
     kp.buf_len = buf_len;   // descriptor bound: the caller's length
@@ -591,7 +721,7 @@ int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mt
     kp.n = n;
     kp.off_shift = off_shift;
     kp.fill_count = ctx->d_count;
-    rc = launch<mg::kTxChunk>(ctx, kp, s.stream);
+    if (rc == MTCP_GPU_OK) rc = launch<mg::kTxChunk>(ctx, kp, s.stream);
     uint32_t cnt = 0;
     if (rc == MTCP_GPU_OK &&
         (!HIP_OK(hipMemcpyAsync(buf, s.d_buf, buf_len, hipMemcpyDeviceToHost, s.stream)) ||

@@ -53,7 +53,9 @@ constexpr int kSlotChunks = 8;           // chunks 0..6 raw (headers), 7 = last 
 constexpr int kRow = 16;                 // lanes per DPP row = lanes per frame
 constexpr int kUnroll = 6;               // loads in flight per row (96 chunks = 1536 B)
 
-enum Mode : int { kRxChunk = 0, kRxPtrs = 1, kTxChunk = 2 };
+// kTxPtrs (tx fill of a pointer burst) runs in rx_wave_kernel only.
+enum Mode : int { kRxChunk = 0, kRxPtrs = 1, kTxChunk = 2, kTxPtrs = 3 };
+constexpr bool is_tx(int m) { return m == kTxChunk || m == kTxPtrs; }
 // Phase-1 schedules (rx_kernel's SCHED; see its comment).  Dispatched:
 // kSchedUnrolled and kSchedSorted; the others are A/B baselines.
 enum Sched : int {
@@ -78,6 +80,9 @@ struct KParams {
     uint32_t rss_nq;
     uint32_t rss_endian;
     uint32_t *fill_count;          // tx fill: frames written (may be null)
+    uint32_t *bins;                // rx: HashFlow bin per packet (may be null)
+    uint2 *tx_report;              // tx (wave kernel): {checks, T} per frame instead of writing them
+    uint32_t rss_key[4];           // key bytes 0..15, big-endian words (wave kernel's Toeplitz)
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -141,6 +146,33 @@ __device__ __forceinline__ uint32_t row_bcast(uint32_t v, int i) {
 #undef MG_NB
 }
 
+// Jenkins one-at-a-time over the 12 key bytes, each read as a signed char
+// (tcp_stream.c:77-87 `char *key`; x86 char is signed).  The bytes of w are
+// key bytes 4q..4q+3 in memory order.
+__device__ __forceinline__ uint32_t hash_flow(const uint32_t (&w)[3]) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        h += (uint32_t)(int32_t)(int8_t)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        h += h << 10;
+        h ^= h >> 6;
+    }
+    h += h << 3;
+    h ^= h >> 11;
+    h += h << 15;
+    return h & (MTCP_GPU_NUM_BINS_FLOWS - 1);
+}
+
+// The flow-table bin of one rx record (f3): HashFlow of the key
+// ProcessTCPPacket hands to StreamHTSearch (tcp_in.c:1180-1186: saddr =
+// iph->daddr, daddr = iph->saddr, sport = tcph->dest, dport = tcph->source),
+// FLOW_NONE for packets that never get there.
+__device__ __forceinline__ uint32_t flow_bin(uint32_t saddr, uint32_t daddr, uint32_t ports,
+                                             uint32_t verdict) {
+    const uint32_t w[3] = {daddr, saddr, (ports >> 16) | (ports << 16)};
+    return verdict == MTCP_GPU_V_TCP_OK ? hash_flow(w) : MTCP_GPU_FLOW_NONE;
+}
+
 // Compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N).
 template <int I0, int N, class F>
 __device__ __forceinline__ void static_for(F &&f) {
@@ -163,6 +195,227 @@ struct WaveLds {
     uint32_t sum[kWave + 1];       // [kWave]: scratch for rows without a frame
     uint4 info[kWave];             // size-sorted schedule: {p16 lo, p16 hi, nch, owner}
 };
+
+// What phase 2 derives for one packet: the record's fields, and for the tx
+// fill the TCP header offset, the IP header's word sum and its check field.
+struct Pkt {
+    uint32_t verdict = MTCP_GPU_V_BAD_DESC;
+    uint32_t eth_type = 0, ip_len = 0, ihl_doff = 0, ip_csum = 0, tcp_csum = 0;
+    uint32_t saddr = 0, daddr = 0, ports = 0, seq = 0, ack = 0, window = 0, flags = 0;
+    uint32_t payload_len = 0;
+    uint32_t T = 0, s_ip = 0, ip_check = 0;
+    bool tcp_entry = false;   // reached the TCP header: the 4-tuple is valid (RSS)
+    bool need_sum = false;    // the segment sum was taken (tx: fill this frame)
+};
+
+// Phase 2 of one packet: the reference's rx chain in its order (eth_in.c:9-56,
+// ip_in.c:15-62, tcp_in.c:1138-1175), ip_fast_csum from the header words and
+// the TCP (or ICMP) checksum from the frame's chunk sum.
+//   raw[i * S], i < 28: dword i of the frame's first seven 16 B chunks on the
+//                       absolute grid (chunk 0 holds the frame's first byte);
+//   raw[(28 + j) * S]:  dword j of its last chunk;
+//   sum:                the sum of the 16-bit halves over all its chunks.
+// The frame starts at any even address p (sh = p & 15 bytes into chunk 0):
+// packet dword i is the funnel of raw dwords a+i and a+i+1 (a = sh / 4) by
+// 8 * (sh & 3) bits, and each 16-bit word of the packet is still a whole
+// half of one aligned dword, which keeps the sum exact.
+// BULK (the wave kernel, wave-uniform operands): the header dwords that the
+// subtraction needs are read from LDS in one batch instead of one
+// conditional read per dword, each of which would wait out the LDS latency.
+template <int MODE, int S, bool BULK = false>
+__device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, uint64_t p,
+                                            uint32_t L, uint32_t nch, bool desc_ok) {
+    Pkt k;
+    const uint32_t sh = (uint32_t)(p & 15);
+    const uint32_t a = sh >> 2, fb = 8 * (sh & 3);
+    auto pd = [&](uint32_t i) -> uint32_t {      // packet dword i (bytes 4i..4i+3)
+        return __builtin_amdgcn_alignbit(raw[(a + i + 1) * S], raw[(a + i) * S], fb);
+    };
+    uint32_t h[19];
+#pragma unroll
+    for (int i = 3; i < 19; ++i) h[i] = pd(i);
+    const uint32_t d0 = h[3];                 // bytes 12..15
+    uint32_t tcp_len = 0, tcheck = 0;
+    bool icmp = false;
+    if (desc_ok) {
+        k.verdict = MTCP_GPU_V_TRUNCATED;
+        if (L >= 14) {
+            k.eth_type = bswap16(d0 & 0xFFFFu);                            // eth_in.c:13
+            if (k.eth_type != 0x0800u) {
+                k.verdict = k.eth_type == 0x0806u ? MTCP_GPU_V_ARP : MTCP_GPU_V_ETH_OTHER;
+            } else if (L >= 18) {
+                k.ip_len = bswap16(h[4] & 0xFFFFu);                        // ip_in.c:21
+                const uint32_t ihl = (d0 >> 16) & 0xFu;
+                k.ihl_doff = ihl;
+                const uint32_t ver = (d0 >> 20) & 0xFu;
+                if (!is_tx(MODE) && k.ip_len < 20) {
+                    k.verdict = MTCP_GPU_V_IP_SHORT;                       // ip_in.c:25-26
+                } else if (L >= 14 + 4 * (ihl > 1 ? ihl : 1)) {
+                    // ip_fast_csum: ihl <= 4 returns dword 0 as is (ps.h:72-73)
+                    uint32_t s_ip = d0 >> 16, lo_last = 0;
+#pragma unroll
+                    for (int j = 1; j < 16; ++j) {
+                        if (j < (int)ihl) s_ip = halves(h[3 + j], s_ip);
+                        if (j == (int)ihl) lo_last = h[3 + j] & 0xFFFFu;
+                    }
+                    s_ip += lo_last;
+                    k.s_ip = s_ip;
+                    k.ip_check = h[6] & 0xFFFFu;
+                    k.ip_csum = ihl <= 4 ? (d0 >> 16) : fold_csum(s_ip);
+                    const uint32_t proto = h[5] >> 24;                     // ip_in.c:52
+                    k.T = 14 + 4 * ihl;
+                    bool tcp_entry = false;
+                    if (is_tx(MODE)) {
+                        tcp_entry = ver == 4 && ihl >= 5 && proto == 6 && L >= k.T + 20;
+                        k.verdict = MTCP_GPU_V_ETH_OTHER;
+                    } else if (k.ip_csum != 0) {
+                        k.verdict = MTCP_GPU_V_IP_CSUM_BAD;                // ip_in.c:35-36
+                    } else if (ver != 4) {
+                        k.verdict = MTCP_GPU_V_IP_VERSION;                 // ip_in.c:47-50
+                    } else if (proto == 1) {
+                        k.verdict = MTCP_GPU_V_ICMP;
+                        // ICMPChecksum(icmph, ip_len - 4*ihl) (icmp.c:18-42), the
+                        // echo-request check of icmp.c:94, when the datagram lies
+                        // inside the frame; a negative length skips the loop: ~0
+                        if (14 + k.ip_len <= L) {
+                            if (k.ip_len >= 4 * ihl) {
+                                icmp = k.need_sum = true;
+                                tcp_len = k.payload_len = k.ip_len - 4 * ihl;
+                            } else {
+                                k.tcp_csum = 0xFFFFu;
+                            }
+                        }
+                    } else if (proto != 6) {
+                        k.verdict = MTCP_GPU_V_IP_PROTO_OTHER;             // ip_in.c:57-59
+                    } else if (L >= k.T + 16) {
+                        tcp_entry = true;
+                    }
+                    if (tcp_entry) {
+                        // tcp_in.c:1142-1149: tcph = iph + 4*ihl
+                        const uint32_t tw = (k.T - 2) >> 2;
+                        const uint32_t e0 = pd(tw), e1 = pd(tw + 1), e2 = pd(tw + 2);
+                        const uint32_t e3 = pd(tw + 3), e4 = pd(tw + 4);
+                        const uint32_t doff = (e3 >> 20) & 0xFu;
+                        k.tcp_entry = true;
+                        k.saddr = (h[6] >> 16) | (h[7] << 16);
+                        k.daddr = (h[7] >> 16) | (h[8] << 16);
+                        k.ports = (e0 >> 16) | (e1 << 16);                 // sport | dport << 16
+                        k.seq = bswap32((e1 >> 16) | (e2 << 16));
+                        k.ack = bswap32((e2 >> 16) | (e3 << 16));
+                        k.window = bswap16(e4 & 0xFFFFu);
+                        k.flags = e3 >> 24;
+                        tcheck = e4 >> 16;
+                        k.ihl_doff = ihl | (doff << 4);
+                        if (is_tx(MODE)) {
+                            if (doff >= 5 && k.ip_len >= 4 * (ihl + doff) && 14 + k.ip_len <= L) {
+                                k.need_sum = true;
+                                tcp_len = k.ip_len - 4 * ihl;
+                            }
+                        } else if (k.ip_len < ((ihl + doff) << 2)) {
+                            k.verdict = MTCP_GPU_V_TCP_LEN_BAD;            // tcp_in.c:1155-1156
+                        } else {
+                            k.payload_len = k.ip_len - ((ihl + doff) << 2);   // tcp_in.c:1144
+                            if (14 + k.ip_len <= L) {
+                                k.need_sum = true;
+                                tcp_len = k.ip_len - 4 * ihl;              // tcp_in.c:1166
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+
+    if (k.need_sum) {
+        // The chunk sum covers [p16, p16 + 16*nch).  Remove the bytes before
+        // the frame, the header bytes [0, T), and everything at or past
+        // E = 14 + ip_len.
+        uint32_t s_out = 0;
+        // (a) bytes [p16, p + T): whole raw dwords, then the low half of the
+        //     next one when sh + T ends mid-dword (T = 14 + 4*ihl is even)
+        const uint32_t nb = sh + k.T;
+        const int whole = (int)(nb >> 2);              // <= (14 + 74) / 4 = 22
+        if constexpr (BULK) {
+            uint32_t rw[23], low = 0;
+#pragma unroll
+            for (int i = 0; i < 23; ++i) rw[i] = raw[i * S];
+#pragma unroll
+            for (int i = 0; i < 23; ++i) {
+                s_out = halves(i < whole ? rw[i] : 0u, s_out);
+                if (i == whole) low = rw[i] & 0xFFFFu;
+            }
+            if (nb & 2) s_out += low;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 28; ++i) {
+                if (i < whole) s_out = halves(raw[i * S], s_out);
+            }
+            if (nb & 2) s_out += raw[whole * S] & 0xFFFFu;
+        }
+        // (b) bytes [p + E, p16 + 16*nch)
+        const uint64_t p16 = p & ~15ull;
+        const uint64_t e_abs = p + 14 + k.ip_len;
+        const uint64_t end = p16 + 16ull * nch;
+        const uint32_t te = (uint32_t)(e_abs & 15);
+        uint64_t cstart = e_abs & ~15ull;                          // chunk holding byte E
+        if (te) {
+            // partial chunk: the last chunk when E and the frame end share it
+            uint4 w;
+            if (cstart + 16 == end) {
+                const uint32_t *t = raw + 4 * (kSlotChunks - 1) * S;
+                w = make_uint4(t[0], t[S], t[2 * S], t[3 * S]);
+            } else {
+                w = gload4(cstart);                                // rare: E well before len
+            }
+            const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int drop = (int)te - 4 * i;   // low bytes inside the segment
+                const uint32_t m = drop <= 0 ? 0xFFFFFFFFu : drop >= 4 ? 0u : (0xFFFFFFFFu << (8 * drop));
+                s_out = halves(wv[i] & m, s_out);
+            }
+            cstart += 16;
+        }
+        for (; cstart < end; cstart += 16) {                       // rare: whole chunks past E
+            const uint4 w = gload4(cstart);
+            s_out = halves(w.w, halves(w.z, halves(w.y, halves(w.x, s_out))));
+        }
+        uint32_t s = sum - s_out;                                  // exact segment sum
+        if (is_tx(MODE)) s -= tcheck;                         // computed with check = 0
+        if (!icmp) {
+            s += (k.saddr & 0xFFFFu) + (k.saddr >> 16);            // tcp_util.c:179-182
+            s += (k.daddr & 0xFFFFu) + (k.daddr >> 16);
+            s += bswap16(tcp_len);
+            s += 0x0600u;                                          // htons(IPPROTO_TCP)
+        }
+        k.tcp_csum = fold_csum(s);                                 // icmp.c:36-38 folds alike
+        if (!is_tx(MODE) && !icmp)
+            k.verdict = k.tcp_csum ? MTCP_GPU_V_TCP_CSUM_BAD : MTCP_GPU_V_TCP_OK;   // tcp_in.c:1167-1173
+    }
+    return k;
+}
+
+// The 40 B record (include/mtcp_gpu.h mtcp_gpu_result) as ten dwords.
+__device__ __forceinline__ void pack_record(const Pkt &k, uint32_t rss_hash, uint32_t rss_queue,
+                                            uint32_t (&r)[10]) {
+    r[0] = k.saddr;
+    r[1] = k.daddr;
+    r[2] = k.ports;
+    r[3] = k.seq;
+    r[4] = k.ack;
+    r[5] = k.window | (k.ip_len << 16);
+    r[6] = k.ip_csum | (k.tcp_csum << 16);
+    r[7] = rss_hash;
+    r[8] = k.payload_len | (k.ihl_doff << 16) | (k.flags << 24);
+    r[9] = k.verdict | (rss_queue << 8) | (k.eth_type << 16);
+}
+
+// util/rss.c:153-165 / mtcp/src/rss.c:90-103: off[m & 3] = {3,1,-1,-3} == m ^ 3
+__device__ __forceinline__ uint32_t rss_core(uint32_t hh, uint32_t nq, uint32_t endian) {
+    uint32_t m = hh & 0x7Fu;
+    if (endian) m ^= 3u;
+    return m % nq;
+}
 
 // A lane's frame: address, length, descriptor validity, and its chunk range
 // [p16, p16 + 16*nch) on the absolute 16 B grid.
@@ -261,7 +514,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         if (f.live) {
             if constexpr (MODE == kRxPtrs) {
                 f.L = raw_b;
-                f.ok = raw_a != 0 && (raw_a & 3) == 0;
+                f.ok = raw_a != 0 && (raw_a & 1) == 0;      // any even start
                 // rows with nothing to read still issue (clamped) loads: keep
                 // their address on always-mapped memory
                 if (f.ok) f.p = raw_a;
@@ -269,7 +522,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                 const uint32_t off = (uint32_t)raw_a;
                 f.L = (uint32_t)(raw_a >> 32) & 0xFFFFu;
                 const int64_t pos = (int64_t)((uint64_t)off << kp.off_shift) - kp.base_sub;
-                f.ok = pos >= 0 && (pos & 3) == 0 && (uint64_t)pos + f.L <= kp.buf_len;
+                f.ok = pos >= 0 && (pos & 1) == 0 && (uint64_t)pos + f.L <= kp.buf_len;
                 if (f.ok) f.p = safe + (uint64_t)pos;
             }
         }
@@ -468,6 +721,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                             *reinterpret_cast<uint2 *>(dst) = make_uint2(v.x, v.y);
                         }
                     }
+                    // f3 fused: the flow-table bin of each held record, computed
+                    // from the record itself (no register held for it), stored
+                    // in runs of B consecutive packets
+                    if (kp.bins) {
+                        const uint32_t rec = gq + map(lane);
+                        if (rec < kp.n)
+                            kp.bins[rec] = flow_bin(keep[q][0], keep[q][1], keep[q][2], keep[q][9] & 0xFFu);
+                    }
                 }
             }
             held = 0;
@@ -537,7 +798,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         fetch(g0 + pass_pkts);                                     // next pass's descriptors
         const uint32_t k = g0 + lane_off;
         const bool live = f.live, desc_ok = f.ok;
-        const uint64_t p = f.p, p16 = f.p16;
+        const uint64_t p = f.p;
         const uint32_t L = f.L, nch = f.nch;
         const bool has_next = g0 + pass_pkts < kp.n;
 
@@ -734,194 +995,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
             continue;
         }
         // ---------------- phase 2: per-lane parse and finish ---------------
-        const uint32_t sh = (uint32_t)(p & 15);
-        const uint32_t *raw = wl.hd + lane;                  // raw dword i at raw[i * kHdStride]
-        const uint32_t *hw = raw + (sh >> 2) * kHdStride;    // packet dword i at hw[i * kHdStride]
-        uint32_t h[24];
+        const Pkt pk = parse_finish<MODE, kHdStride>(wl.hd + lane, wl.sum[lane], p, L, nch, desc_ok);
+        uint32_t rss_hash = 0, rss_queue = 0;
+        if constexpr (RSS) {
+            if (pk.tcp_entry) {
+                // util/rss.c:107-145 as 24 nibble tables: the input bytes
+                // (sip, dip, sp, dp host order, MSB first) are saddr/daddr/ports
+                // in memory order.
+                uint32_t hh = 0;
 #pragma unroll
-        for (int i = 0; i < 24; ++i) h[i] = hw[i * kHdStride];
-
-        uint32_t verdict = MTCP_GPU_V_BAD_DESC;
-        uint32_t eth_type = 0, ip_len = 0, ihl = 0, ihl_doff = 0, ip_csum = 0;
-        uint32_t saddr = 0, daddr = 0, ports = 0, seq = 0, ack = 0, window = 0, flags = 0;
-        uint32_t payload_len = 0, rss_hash = 0, rss_queue = 0;
-        uint32_t tcp_len = 0, T = 0, s_ip = 0, tcheck = 0, tcp_csum = 0;
-        bool need_sum = false, icmp = false;
-        const uint32_t d0 = h[3];                 // bytes 12..15
-        if (desc_ok) {
-            verdict = MTCP_GPU_V_TRUNCATED;
-            if (L >= 14) {
-                eth_type = bswap16(d0 & 0xFFFFu);                          // eth_in.c:13
-                if (eth_type != 0x0800u) {
-                    verdict = eth_type == 0x0806u ? MTCP_GPU_V_ARP : MTCP_GPU_V_ETH_OTHER;
-                } else if (L >= 18) {
-                    ip_len = bswap16(h[4] & 0xFFFFu);                      // ip_in.c:21
-                    ihl = (d0 >> 16) & 0xFu;
-                    ihl_doff = ihl;
-                    const uint32_t ver = (d0 >> 20) & 0xFu;
-                    if (MODE != kTxChunk && ip_len < 20) {
-                        verdict = MTCP_GPU_V_IP_SHORT;                     // ip_in.c:25-26
-                    } else if (L >= 14 + 4 * (ihl > 1 ? ihl : 1)) {
-                        // ip_fast_csum: ihl <= 4 returns dword 0 as is (ps.h:72-73)
-                        s_ip = d0 >> 16;
-                        uint32_t lo_last = 0;
-#pragma unroll
-                        for (int j = 1; j < 16; ++j) {
-                            if (j < (int)ihl) s_ip = halves(h[3 + j], s_ip);
-                            if (j == (int)ihl) lo_last = h[3 + j] & 0xFFFFu;
-                        }
-                        s_ip += lo_last;
-                        ip_csum = ihl <= 4 ? (d0 >> 16) : fold_csum(s_ip);
-                        const uint32_t proto = h[5] >> 24;                 // ip_in.c:52
-                        T = 14 + 4 * ihl;
-                        bool tcp_entry = false;
-                        if (MODE == kTxChunk) {
-                            tcp_entry = ver == 4 && ihl >= 5 && proto == 6 && L >= T + 20;
-                            verdict = MTCP_GPU_V_ETH_OTHER;
-                        } else if (ip_csum != 0) {
-                            verdict = MTCP_GPU_V_IP_CSUM_BAD;              // ip_in.c:35-36
-                        } else if (ver != 4) {
-                            verdict = MTCP_GPU_V_IP_VERSION;               // ip_in.c:47-50
-                        } else if (proto == 1) {
-                            verdict = MTCP_GPU_V_ICMP;
-                            // ICMPChecksum(icmph, ip_len - 4*ihl) (icmp.c:18-42),
-                            // the echo-request check of icmp.c:94, when the
-                            // datagram lies inside the frame; a negative length
-                            // skips the loop: ~0
-                            if (14 + ip_len <= L) {
-                                if (ip_len >= 4 * ihl) {
-                                    icmp = need_sum = true;
-                                    tcp_len = payload_len = ip_len - 4 * ihl;
-                                } else {
-                                    tcp_csum = 0xFFFFu;
-                                }
-                            }
-                        } else if (proto != 6) {
-                            verdict = MTCP_GPU_V_IP_PROTO_OTHER;           // ip_in.c:57-59
-                        } else if (L >= T + 16) {
-                            tcp_entry = true;
-                        }
-                        if (tcp_entry) {
-                            // tcp_in.c:1142-1149: tcph = iph + 4*ihl
-                            const uint32_t tw = (T - 2) >> 2;
-                            const uint32_t *te = hw + tw * kHdStride;
-                            const uint32_t e0 = te[0], e1 = te[kHdStride], e2 = te[2 * kHdStride];
-                            const uint32_t e3 = te[3 * kHdStride], e4 = te[4 * kHdStride];
-                            const uint32_t doff = (e3 >> 20) & 0xFu;
-                            saddr = (h[6] >> 16) | (h[7] << 16);
-                            daddr = (h[7] >> 16) | (h[8] << 16);
-                            ports = (e0 >> 16) | (e1 << 16);               // sport | dport << 16
-                            seq = bswap32((e1 >> 16) | (e2 << 16));
-                            ack = bswap32((e2 >> 16) | (e3 << 16));
-                            window = bswap16(e4 & 0xFFFFu);
-                            flags = e3 >> 24;
-                            tcheck = e4 >> 16;
-                            ihl_doff = ihl | (doff << 4);
-                            if constexpr (RSS) {
-                                // util/rss.c:107-145 as 24 nibble tables: the input
-                                // bytes (sip, dip, sp, dp host order, MSB first)
-                                // are saddr/daddr/ports in memory order.
-                                uint32_t hh = 0;
-#pragma unroll
-                                for (int b = 0; b < 4; ++b) {
-                                    const uint32_t sb = (saddr >> (8 * b)) & 0xFFu;
-                                    const uint32_t db = (daddr >> (8 * b)) & 0xFFu;
-                                    const uint32_t pb = (ports >> (8 * b)) & 0xFFu;
-                                    hh ^= rss_lds[((2 * b) << 4) | (sb >> 4)] ^
-                                          rss_lds[((2 * b + 1) << 4) | (sb & 15)];
-                                    hh ^= rss_lds[((8 + 2 * b) << 4) | (db >> 4)] ^
-                                          rss_lds[((9 + 2 * b) << 4) | (db & 15)];
-                                    hh ^= rss_lds[((16 + 2 * b) << 4) | (pb >> 4)] ^
-                                          rss_lds[((17 + 2 * b) << 4) | (pb & 15)];
-                                }
-                                rss_hash = hh;
-                                // util/rss.c:153-165: off[m & 3] = {3,1,-1,-3} == m ^ 3
-                                uint32_t m = hh & 0x7Fu;
-                                if (kp.rss_endian) m ^= 3u;
-                                rss_queue = m % kp.rss_nq;
-                            }
-                            if (MODE == kTxChunk) {
-                                if (doff >= 5 && ip_len >= 4 * (ihl + doff) && 14 + ip_len <= L) {
-                                    need_sum = true;
-                                    tcp_len = ip_len - 4 * ihl;
-                                }
-                            } else if (ip_len < ((ihl + doff) << 2)) {
-                                verdict = MTCP_GPU_V_TCP_LEN_BAD;          // tcp_in.c:1155-1156
-                            } else {
-                                payload_len = ip_len - ((ihl + doff) << 2);   // tcp_in.c:1144
-                                if (14 + ip_len <= L) {
-                                    need_sum = true;
-                                    tcp_len = ip_len - 4 * ihl;              // tcp_in.c:1166
-                                }
-                            }
-                        }
-                    }
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t sb = (pk.saddr >> (8 * b)) & 0xFFu;
+                    const uint32_t db = (pk.daddr >> (8 * b)) & 0xFFu;
+                    const uint32_t pb = (pk.ports >> (8 * b)) & 0xFFu;
+                    hh ^= rss_lds[((2 * b) << 4) | (sb >> 4)] ^ rss_lds[((2 * b + 1) << 4) | (sb & 15)];
+                    hh ^= rss_lds[((8 + 2 * b) << 4) | (db >> 4)] ^ rss_lds[((9 + 2 * b) << 4) | (db & 15)];
+                    hh ^= rss_lds[((16 + 2 * b) << 4) | (pb >> 4)] ^ rss_lds[((17 + 2 * b) << 4) | (pb & 15)];
                 }
+                rss_hash = hh;
+                rss_queue = rss_core(hh, kp.rss_nq, kp.rss_endian);
             }
-        }
-
-        if (need_sum) {
-            // The chunk sum covers [p16, p16 + 16*nch).  Remove the bytes before
-            // the frame, the header bytes [0, T), and everything at or past
-            // E = 14 + ip_len.
-            uint32_t s_out = 0;
-            // (a) raw dwords before the frame (sh/4 of them) and header dwords
-            //     0 .. (T-2)/4 - 1, plus the low half of dword (T-2)/4
-            const int pre = (int)(sh >> 2);
-            const int tw = pre + (int)((T - 2) >> 2);
-#pragma unroll
-            for (int i = 0; i < 28; ++i) {
-                if (i < tw) s_out = halves(raw[i * kHdStride], s_out);
-            }
-            s_out += raw[tw * kHdStride] & 0xFFFFu;
-            // (b) bytes [p + E, p16 + 16*nch)
-            const uint64_t e_abs = p + 14 + ip_len;
-            const uint64_t end = p16 + 16ull * nch;
-            const uint32_t te = (uint32_t)(e_abs & 15);
-            uint64_t cstart = e_abs & ~15ull;                      // chunk holding byte E
-            if (te) {
-                // partial chunk: the last chunk when E and the frame end share it
-                uint4 w;
-                if (cstart + 16 == end) {
-                    const uint32_t *t = raw + 4 * (kSlotChunks - 1) * kHdStride;
-                    w = make_uint4(t[0], t[kHdStride], t[2 * kHdStride], t[3 * kHdStride]);
-                } else {
-                    w = gload4(cstart);                            // rare: E well before len
-                }
-                const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int drop = (int)te - 4 * i;   // low bytes inside the segment
-                    const uint32_t m = drop <= 0 ? 0xFFFFFFFFu : drop >= 4 ? 0u : (0xFFFFFFFFu << (8 * drop));
-                    s_out = halves(wv[i] & m, s_out);
-                }
-                cstart += 16;
-            }
-            for (; cstart < end; cstart += 16) {                   // rare: whole chunks past E
-                const uint4 w = gload4(cstart);
-                s_out = halves(w.w, halves(w.z, halves(w.y, halves(w.x, s_out))));
-            }
-            uint32_t s = wl.sum[lane] - s_out;                     // exact segment sum
-            if (MODE == kTxChunk) s -= tcheck;                     // computed with check = 0
-            if (!icmp) {
-                s += (saddr & 0xFFFFu) + (saddr >> 16);            // tcp_util.c:179-182
-                s += (daddr & 0xFFFFu) + (daddr >> 16);
-                s += bswap16(tcp_len);
-                s += 0x0600u;                                      // htons(IPPROTO_TCP)
-            }
-            tcp_csum = fold_csum(s);                               // icmp.c:36-38 folds alike
-            if (MODE != kTxChunk && !icmp)
-                verdict = tcp_csum ? MTCP_GPU_V_TCP_CSUM_BAD : MTCP_GPU_V_TCP_OK;   // tcp_in.c:1167-1173
         }
 
         if constexpr (MODE == kTxChunk) {
             uint32_t fill[4] = {0, 0, 0, 0};                        // {p lo, p hi, checks, T}
-            if (live && need_sum) {
-                const uint32_t ipc = fold_csum(s_ip - (h[6] & 0xFFFFu));   // ip_out.c:145,164
+            if (live && pk.need_sum) {
+                const uint32_t ipc = fold_csum(pk.s_ip - pk.ip_check);   // ip_out.c:145,164
                 fill[0] = (uint32_t)p;
                 fill[1] = (uint32_t)(p >> 32);
-                fill[2] = ipc | (tcp_csum << 16);
-                fill[3] = T;
+                fill[2] = ipc | (pk.tcp_csum << 16);
+                fill[3] = pk.T;
                 if (kp.fill_count) atomicAdd(kp.fill_count, 1u);
             }
             if constexpr (kTxDefer > 0) {
@@ -929,29 +1032,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
             } else {
                 tx_write(fill);
             }
-        } else if constexpr (kDefer > 0) {
-            const uint32_t r[10] = {saddr, daddr, ports, seq, ack, window | (ip_len << 16),
-                                    ip_csum | (tcp_csum << 16), rss_hash,
-                                    payload_len | (ihl_doff << 16) | (flags << 24),
-                                    verdict | (rss_queue << 8) | (eth_type << 16)};
-            push(r, g0);
         } else {
-            // stage the 64 records (2560 B) in this wave's LDS, then store
-            // them as 8-byte pieces: lanes of one run of B packets write one
-            // contiguous B*40-byte span of the output
-            uint2 *st = reinterpret_cast<uint2 *>(wl.hd) + lane * 5;
-            st[0] = make_uint2(saddr, daddr);
-            st[1] = make_uint2(ports, seq);
-            st[2] = make_uint2(ack, window | (ip_len << 16));
-            st[3] = make_uint2(ip_csum | (tcp_csum << 16), rss_hash);
-            st[4] = make_uint2(payload_len | (ihl_doff << 16) | (flags << 24),
-                               verdict | (rss_queue << 8) | (eth_type << 16));
-            const uint2 *src = reinterpret_cast<const uint2 *>(wl.hd);
+            uint32_t r[10];
+            pack_record(pk, rss_hash, rss_queue, r);
+            if constexpr (kDefer > 0) {
+                push(r, g0);
+            } else {
+                // stage the 64 records (2560 B) in this wave's LDS, then store
+                // them as 8-byte pieces: lanes of one run of B packets write one
+                // contiguous B*40-byte span of the output
+                uint2 *st = reinterpret_cast<uint2 *>(wl.hd) + lane * 5;
 #pragma unroll
-            for (uint32_t i = 0; i < 5; ++i) {
-                const uint32_t q = i * kWave + lane;      // 8-byte piece of record q/5
-                const uint32_t rec = g0 + map(q / 5);
-                if (rec < kp.n) reinterpret_cast<uint2 *>(kp.out + rec)[q % 5] = src[q];
+                for (int i = 0; i < 5; ++i) st[i] = make_uint2(r[2 * i], r[2 * i + 1]);
+                const uint2 *src = reinterpret_cast<const uint2 *>(wl.hd);
+#pragma unroll
+                for (uint32_t i = 0; i < 5; ++i) {
+                    const uint32_t q = i * kWave + lane;      // 8-byte piece of record q/5
+                    const uint32_t rec = g0 + map(q / 5);
+                    if (rec < kp.n) reinterpret_cast<uint2 *>(kp.out + rec)[q % 5] = src[q];
+                }
+                if (kp.bins && live) kp.bins[k] = flow_bin(r[0], r[1], r[2], r[9] & 0xFFu);
             }
         }
     }

@@ -103,6 +103,20 @@ class Context:
         check(lib().mtcp_gpu_rx_ptrs_dev(self._h, _dptr(ptrs), _dptr(lens), n, _dptr(out),
                                          _stream_handle(stream)), "mtcp_gpu_rx_ptrs_dev")
 
+    def rx_chunk_flow_dev(self, buf, desc, n: int, off_shift: int, out, bins, stream=None) -> None:
+        check(lib().mtcp_gpu_rx_chunk_flow_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
+                                               _dptr(desc), n, off_shift, _dptr(out), _dptr(bins),
+                                               _stream_handle(stream)), "mtcp_gpu_rx_chunk_flow_dev")
+
+    def rx_ptrs_flow_dev(self, ptrs, lens, n: int, out, bins, stream=None) -> None:
+        check(lib().mtcp_gpu_rx_ptrs_flow_dev(self._h, _dptr(ptrs), _dptr(lens), n, _dptr(out),
+                                              _dptr(bins), _stream_handle(stream)),
+              "mtcp_gpu_rx_ptrs_flow_dev")
+
+    def tx_fill_ptrs_dev(self, ptrs, lens, n: int, stream=None) -> None:
+        check(lib().mtcp_gpu_tx_fill_ptrs_dev(self._h, _dptr(ptrs), _dptr(lens), n,
+                                              _stream_handle(stream)), "mtcp_gpu_tx_fill_ptrs_dev")
+
     def tx_fill_dev(self, buf, desc, n: int, off_shift: int, stream=None) -> None:
         check(lib().mtcp_gpu_tx_fill_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
                                          _dptr(desc), n, off_shift, _stream_handle(stream)),
@@ -135,6 +149,19 @@ class Context:
                                      len(desc), off_shift, ctypes.byref(cnt)), "mtcp_gpu_tx_fill")
         return cnt.value
 
+
+    def tx_fill_ptrs(self, buf: np.ndarray, offsets, lens) -> int:
+        """mtcp_gpu_tx_fill_ptrs over frames of the host array `buf` at byte
+        `offsets` (a DPDK-style pointer burst into one host buffer); fills
+        `buf` in place and returns the number of frames filled."""
+        offsets = np.asarray(offsets, dtype=np.int64)
+        n = len(offsets)
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[buf.ctypes.data + int(o) for o in offsets])
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        cnt = ctypes.c_uint32(0)
+        check(lib().mtcp_gpu_tx_fill_ptrs(self._h, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data,
+                                          n, ctypes.byref(cnt)), "mtcp_gpu_tx_fill_ptrs")
+        return cnt.value
 
     # -- flow-table hash (HashFlow, mtcp/src/tcp_stream.c:56-90) -------------
     def flow_hash_dev(self, res, n: int, bins, stream=None) -> None:

@@ -278,7 +278,7 @@ static int desc_bad(uint64_t buf_len, const mtcp_gpu_desc *d, uint32_t off_shift
 {
     uint64_t p = (uint64_t)d->offset << off_shift;
     *pos = p;
-    return (p & 3) != 0 || p + d->len > buf_len;
+    return (p & 1) != 0 || p + d->len > buf_len;      /* any even start (include/mtcp_gpu.h) */
 }
 
 void oracle_rx_chunk(const uint8_t *buf, uint64_t buf_len, const mtcp_gpu_desc *desc,

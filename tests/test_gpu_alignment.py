@@ -1,4 +1,4 @@
-"""Frames at every 4-byte alignment inside a 128 B line, through each phase-1
+"""Frames at every 2-byte alignment inside a 128 B line, through each phase-1
 schedule the library dispatches (mtcp_gpu.hip launch_sched): size-sorted
 rounds (average slot < 1 KiB, or <= 1536 B in batches of at most 64 K
 packets), unrolled rounds (<= 1536 B in larger batches) and unrolled
@@ -36,7 +36,7 @@ def _lengths(kind, n, rng):
 
 
 def _unaligned_batch(kind, n=1536, seed=11):
-    """Generator frames re-packed so that frame i starts at 4*(i % 32) mod 128."""
+    """Generator frames re-packed so that frame i starts at 2*(i % 64) mod 128."""
     rng = np.random.default_rng(seed)
     lens = _lengths(kind, n, rng).astype(np.uint16)
     desc64, nbytes = pktgen.layout_from_lengths(lens, 6)
@@ -46,7 +46,7 @@ def _unaligned_batch(kind, n=1536, seed=11):
     pos = 0
     for i in range(n):
         pos = (pos + 127) & ~127                     # next line, then the alignment under test
-        offs[i] = pos + 4 * (i % 32)
+        offs[i] = pos + 2 * (i % 64)
         pos = offs[i] + int(lens[i])
     buf = np.zeros(((pos + 127) & ~127) + 128, np.uint8)
     s0 = desc64["offset"].astype(np.int64) << 6
@@ -65,7 +65,8 @@ def _unaligned_batch(kind, n=1536, seed=11):
                                                     ("mid", 1024, 1536, (1 << 16) + 512),
                                                     ("mid", 1024, 1536, 1536),
                                                     ("small", 0, 1023, 1536)])
-def test_unaligned_frames_every_schedule(gpu, kind, slot_lo, slot_hi, n):
+def test_unaligned_frames_every_schedule(gpu, kind, slot_lo, slot_hi, n, monkeypatch):
+    monkeypatch.setenv("MTCP_GPU_WAVE_UPTO", "0")      # rx_kernel's schedules (test_gpu_wave: the wave kernel)
     buf, desc = _unaligned_batch(kind, n)
     padded = buf.nbytes + (-buf.nbytes) % 16
     assert slot_lo <= padded // len(desc) <= slot_hi        # the schedule under test is dispatched
@@ -94,7 +95,7 @@ def test_unaligned_frames_pointer_burst(gpu):
 
 def test_maximum_length_frames(gpu):
     """Frames up to the u16 maximum (65 535 B: 43 trips, tot_len 65 521, a TCP
-    sum of 32 760 words — still exact in 32 bits), at odd 4-byte alignments,
+    sum of 32 760 words — still exact in 32 bits), at odd 2-byte alignments,
     with and without a flipped payload bit; chunk mode and pointer burst."""
     lens = np.array([65535, 65534, 65533, 40001, 16385, 9001, 1537, 65535] * 4, dtype=np.uint16)
     n = len(lens)
@@ -103,7 +104,7 @@ def test_maximum_length_frames(gpu):
     oracle.pktgen(src, desc64, 6, 21, 0)
     offs, pos = np.zeros(n, np.int64), 0
     for i in range(n):
-        pos = ((pos + 127) & ~127) + 4 * (7 * i % 32)
+        pos = ((pos + 127) & ~127) + 2 * (7 * i % 64)
         offs[i] = pos
         pos += int(lens[i])
     buf = np.zeros(((pos + 127) & ~127) + 128, np.uint8)

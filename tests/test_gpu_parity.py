@@ -184,15 +184,17 @@ def test_rss_microsoft_key_nq16_no_endian(gpu):
 def test_edge_descriptors(gpu, golden):
     buf = golden.buf[:1 << 16].copy()
     d = np.zeros(7, dtype=DESC_DTYPE)
-    d["offset"] = [0, 2, 65536 - 64, 65536, 1 << 31, 64, 130]
+    d["offset"] = [0, 3, 65536 - 64, 65536, 1 << 31, 64, 130]
     d["len"] = [64, 64, 64, 64, 64, 0, 60]
     with gpu.Context(0) as ctx:
         got = run_rx_dev(ctx, buf, d, 0)
         assert ctx.rx_chunk(buf, d[:0], 0).shape == (0,)
     want = oracle.rx_chunk(buf, d, 0)
     assert_same(got, want, "edges")
+    # odd start, past the chunk, offset overflow: BAD_DESC; an even start is read
     assert got["verdict"][1] == V_BAD_DESC and got["verdict"][3] == V_BAD_DESC
     assert got["verdict"][4] == V_BAD_DESC and got["verdict"][5] == V_TRUNCATED
+    assert got["verdict"][6] != V_BAD_DESC
 
 
 def test_rx_unsorted_host_path(gpu, golden):
@@ -216,12 +218,13 @@ def test_rx_is_read_only(gpu, golden):
 
 
 # ---- BASELINE.json full sizes: size-independent properties -----------------
-def _expected_verdicts(n, seed, lens):
+def _expected_verdicts(n, seed, lens, first_index=0):
     """Verdict each generated frame must get, from the generator's own rule
     (include/mtcp_gpu_pktgen.h): bit flips in the IP header -> IP_CSUM_BAD,
-    else in the TCP segment -> TCP_CSUM_BAD, else TCP_OK."""
+    else in the TCP segment -> TCP_CSUM_BAD, else TCP_OK.  Packet i of the
+    batch is global packet first_index + i."""
     with np.errstate(over="ignore"):
-        i = np.arange(n, dtype=np.uint64)
+        i = np.arange(first_index, first_index + n, dtype=np.uint64)
         mix = pktgen._mix
         s = mix(np.uint64(seed) ^ (i * np.uint64(0xD1342543DE82EF95) + np.uint64(0x632BE59BD9B4E019)))
         c = mix(s + np.uint64(7) * np.uint64(0x9E3779B97F4A7C15))

@@ -1,0 +1,111 @@
+"""The multi-GPU batch split (SURVEY §8 e) on the device.
+
+* C4's per-GPU shard — 2 M x 1500 B of a 16 M batch over 8 GPUs, generated
+  from its global packet indices — runs as two launches of rx_kernel's
+  unrolled schedule (mtcp_gpu.hip launch: 1 M packets per launch on a full
+  MI355X).  Every packet's verdict is the one the generator's corruption
+  rule predicts, and a 1 % sample plus every record within 64 packets of the
+  launch boundary equal the oracle's.  Ranks 0 and 7 (first and last shard).
+* bench.py's N > 1 path itself (torch.distributed.run, gloo, shard /
+  generate / rx / barriers) with two ranks sharing device 0
+  (MTCP_BENCH_DEVICE=0): the records the ranks dump, concatenated, equal one
+  launch over the whole batch.  The CPU analogue of the split is mTCP's
+  per-core RSS queues (mtcp/src/dpdk_module.c:644-676).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from mtcp_amd import RESULT_DTYPE, pktgen, shard
+from tests.test_gpu_parity import DEV, V_TCP_OK, _expected_verdicts, assert_same, dev_results, to_dev
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    from mtcp_amd import gpu as g
+    return g
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c4_shard_two_launches(gpu, rank):
+    seed, world = 4, 8
+    sh = shard.make_shard(1 << 24, 1500, rank, world, seed)
+    n = sh.count
+    assert n == 1 << 21 and sh.first_index == rank * n
+    b = torch.empty(sh.nbytes, dtype=torch.uint8, device=DEV)
+    d = to_dev(sh.desc)
+    gpu.pktgen_dev(b, d, n, 6, seed, sh.first_index)
+    out = dev_results(n)
+    with gpu.Context(0) as ctx:
+        ctx.rx_chunk_dev(b, d, n, 6, out)
+        torch.cuda.synchronize()
+    got = out.cpu().numpy().view(RESULT_DTYPE)
+    want_v, ip_flip = _expected_verdicts(n, seed, sh.desc["len"], first_index=sh.first_index)
+    ok = ~ip_flip
+    assert np.array_equal(got["verdict"][ok], want_v[ok])
+    assert np.all(got["verdict"][ip_flip] != V_TCP_OK)
+    launch = 256 * 2 * 4 * 64 * 8          # packets per launch on 256 CUs (mtcp_gpu.hip kHeldPasses)
+    rng = np.random.default_rng(rank)
+    idx = np.unique(np.concatenate([rng.choice(n, size=n // 100, replace=False),
+                                    np.arange(launch - 64, launch + 64), np.arange(64),
+                                    np.arange(n - 64, n)]))
+    host = b.cpu().numpy()
+    assert_same(got[idx], oracle.rx_chunk(host, sh.desc[idx], 6), f"c4 shard {rank}")
+
+
+def _bench_ranks(tmp_path, config, per_gpu, world=2):
+    dump = tmp_path / config
+    env = dict(os.environ, MTCP_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    port = 29600 + os.getpid() % 300
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--config", config, "--per-gpu", str(per_gpu), "--steps", "3",
+           "--warmup", "1", "--cpu-baseline", "off", "--pcie", "off", "--dump-records", str(dump)]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    recs, metas = [], []
+    for r in range(world):
+        metas.append(json.load(open(dump / f"shard_rank{r}.json")))
+        recs.append(np.fromfile(dump / f"records_rank{r}.bin", dtype=RESULT_DTYPE))
+    return line, metas, recs
+
+
+@pytest.mark.parametrize("config,size,rss,per_gpu", [("c2", 1500, False, 1 << 17),
+                                                     ("c3", "bimodal", True, 1 << 17)])
+def test_bench_two_ranks_equal_one_launch(gpu, tmp_path, config, size, rss, per_gpu):
+    line, metas, recs = _bench_ranks(tmp_path, config, per_gpu)
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["config"]["packets_total"] == 2 * per_gpu
+    first = 0
+    for m, r in zip(metas, recs):
+        assert m["first_index"] == first and m["count"] == len(r)
+        first += m["count"]
+    assert first == 2 * per_gpu
+    seed = {"c2": 2, "c3": 3}[config]
+    n = 2 * per_gpu
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    d = to_dev(desc)
+    gpu.pktgen_dev(b, d, n, 6, seed)
+    out = dev_results(n)
+    kw = dict(rss=True, rss_queues=8, rss_endian=True) if rss else {}
+    with gpu.Context(0, **kw) as ctx:
+        ctx.rx_chunk_dev(b, d, n, 6, out)
+        torch.cuda.synchronize()
+    whole = out.cpu().numpy().view(RESULT_DTYPE)
+    assert_same(np.concatenate(recs), whole, f"{config} ranks vs one launch")
+    if size == "bimodal":                  # the byte-balanced split of shard.bounds
+        cut = metas[1]["first_index"]
+        assert cut == shard.bounds(n, size, 2, seed)[1]

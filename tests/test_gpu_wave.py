@@ -1,0 +1,246 @@
+"""Small batches and the entry points added with the wave-per-packet kernel
+(mtcp_amd/csrc/rx_wave.hpp), on the MI355X, bit-exact:
+
+* every dispatched schedule — the wave kernel (batches of at most
+  kWaveUpToPkts packets, mtcp_gpu.hip) and rx_kernel's sorted / unrolled /
+  line-aligned rounds (forced with MTCP_GPU_WAVE_UPTO=0) — on the golden
+  vectors and on config-shaped batches of 4 096 (one io_module aggregate)
+  and 65 536 packets, against the reference's results and the oracle;
+* frames at every even start (2-byte aligned, NET_IP_ALIGN-style), chunk and
+  pointer modes, rx and tx;
+* rx with HashFlow fused in (mtcp_gpu_rx_*_flow_dev) against the reference's
+  own bins (tests/golden/rx_flowbins.bin) and the separate f3 kernel;
+* the tx fill of pointer bursts (mtcp_gpu_tx_fill_ptrs[_dev]) against the
+  reference's fills;
+* mtcp_gpu_reserve(0, 0) / rxq creation on a context that already ran host
+  calls (the staging it warms is then already allocated).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from mtcp_amd import RESULT_DTYPE, pktgen
+from tests.golden_io import compare_results
+from tests.repack import repack
+from tests.test_gpu_parity import DEV, assert_same, dev_results, run_rx_dev, to_dev
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+WAVE_UPTO = 1 << 15          # mtcp_gpu.hip kWaveUpToPkts
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    from mtcp_amd import gpu as g
+    return g
+
+
+def ctx_for(gpu, monkeypatch, sched, **kw):
+    """A context whose small batches take `sched`: "wave" (every batch size) or
+    "rows" (rx_kernel's schedules only)."""
+    monkeypatch.setenv("MTCP_GPU_WAVE_UPTO", str(1 << 31) if sched == "wave" else "0")
+    c = gpu.Context(0, **kw)
+    monkeypatch.delenv("MTCP_GPU_WAVE_UPTO")
+    return c
+
+
+def ptr_burst(b, desc):
+    ptrs = torch.from_numpy(desc["offset"].astype(np.int64) + b.data_ptr()).to(DEV)
+    lens = torch.from_numpy(desc["len"].view(np.int16).copy()).to(DEV)
+    return ptrs, lens
+
+
+SCHEDS = ["wave", "rows"]
+
+
+@pytest.mark.parametrize("sched", SCHEDS)
+def test_golden_every_schedule(gpu, golden, monkeypatch, sched):
+    rss = oracle.rss_cfg(oracle.KEY_0X05, golden.rss_num_queues, 1)
+    want = oracle.rx_chunk(golden.buf, golden.desc, 0, rss)
+    n = len(golden.desc)
+    with ctx_for(gpu, monkeypatch, sched, rss=True, rss_queues=golden.rss_num_queues) as ctx:
+        got = run_rx_dev(ctx, golden.buf, golden.desc, 0)
+        b = to_dev(golden.buf)
+        ptrs, lens = ptr_burst(b, golden.desc)
+        out = dev_results(n)
+        ctx.rx_ptrs_dev(ptrs, lens, n, out)
+        torch.cuda.synchronize()
+        got_p = out.cpu().numpy().view(RESULT_DTYPE)
+        d = to_dev(golden.desc)
+        ctx.tx_fill_dev(b, d, n, 0)
+        torch.cuda.synchronize()
+        filled = b.cpu().numpy()
+    bad = compare_results(got, golden)
+    assert not bad, bad
+    assert_same(got, want, f"{sched} chunk vs oracle")
+    assert not compare_results(got_p, golden)
+    assert_same(got_p, want, f"{sched} pointers vs oracle")
+    fixed = golden.buf.copy()
+    assert oracle.tx_fill(fixed, golden.desc, 0) == golden.manifest["tx_filled"]
+    assert np.array_equal(filled, fixed)
+
+
+@pytest.mark.parametrize("n", [4096, 1 << 16])
+@pytest.mark.parametrize("size,rss", [(1500, False), ("bimodal", True), (64, False), (9000, False)])
+def test_small_batches_every_schedule(gpu, monkeypatch, n, size, rss):
+    """One io_module aggregate (4 096 frames) and 64 K frames: the wave kernel
+    and rx_kernel's schedule for the same batch, both equal to the oracle."""
+    if size == 9000 and n > 4096:
+        n = 16384
+    seed = 61
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(None, 8, 1) if rss else None)
+    kw = dict(rss=True, rss_queues=8, rss_endian=True) if rss else {}
+    for sched in SCHEDS:
+        with ctx_for(gpu, monkeypatch, sched, **kw) as ctx:
+            assert_same(run_rx_dev(ctx, buf, desc, 6), want, f"{sched} {size} x {n}")
+    assert (want["verdict"] == 0).mean() > 0.99
+
+
+@pytest.mark.parametrize("key,nq,endian", [(None, 8, 1), ("ms", 16, 0), ("ms", 5, 1)])
+def test_wave_toeplitz_both_keys(gpu, monkeypatch, key, nq, endian):
+    """The wave kernel's lane-parallel Toeplitz (key windows from the key
+    words, no table) for both keys of util/rss.c."""
+    k = oracle.KEY_MICROSOFT if key == "ms" else None
+    n, seed = 8192, 62
+    desc, nbytes = pktgen.layout(n, "bimodal", 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(k, nq, endian))
+    with ctx_for(gpu, monkeypatch, "wave", rss=True, rss_key=k, rss_queues=nq,
+                 rss_endian=bool(endian)) as ctx:
+        got = run_rx_dev(ctx, buf, desc, 6)
+    assert_same(got, want, f"toeplitz key={key} nq={nq} endian={endian}")
+    assert len(np.unique(got["rss_queue"])) == nq
+
+
+def _even_phase(i):
+    return (2 * i) % 128
+
+
+@pytest.mark.parametrize("sched", SCHEDS)
+def test_golden_at_every_even_start(gpu, golden, monkeypatch, sched):
+    """The golden frames at every 2-byte alignment inside a 128 B line: the
+    reference's records (chunk and pointer modes) and its tx fills."""
+    buf, desc = repack(golden.buf, golden.desc, 0, _even_phase)
+    n = len(desc)
+    with ctx_for(gpu, monkeypatch, sched, rss=True, rss_queues=golden.rss_num_queues) as ctx:
+        got = run_rx_dev(ctx, buf, desc, 0)
+        b = to_dev(buf)
+        ptrs, lens = ptr_burst(b, desc)
+        out = dev_results(n)
+        ctx.rx_ptrs_dev(ptrs, lens, n, out)
+        ctx.tx_fill_dev(b, to_dev(desc), n, 0)
+        torch.cuda.synchronize()
+        got_p = out.cpu().numpy().view(RESULT_DTYPE)
+        filled = b.cpu().numpy()
+    assert not compare_results(got, golden), compare_results(got, golden)
+    assert not compare_results(got_p, golden), compare_results(got_p, golden)
+    want_fill = buf.copy()
+    oracle.tx_fill(want_fill, desc, 0)
+    assert np.array_equal(filled, want_fill)
+    # odd starts are refused
+    d = desc[:64].copy()
+    d["offset"] += 1
+    with ctx_for(gpu, monkeypatch, sched) as ctx:
+        assert (run_rx_dev(ctx, buf, d, 0)["verdict"] == 11).all()
+
+
+@pytest.mark.parametrize("sched", SCHEDS)
+def test_fused_flow_bins_golden(gpu, golden, monkeypatch, sched):
+    """rx + HashFlow in one launch: the reference's bins for the golden chunk
+    (HashFlow over the keys it handed to StreamHTSearch, golden_flow.c)."""
+    n = len(golden.desc)
+    b = to_dev(golden.buf)
+    d = to_dev(golden.desc)
+    with ctx_for(gpu, monkeypatch, sched, rss=True, rss_queues=golden.rss_num_queues) as ctx:
+        out = dev_results(n)
+        bins = torch.full((n,), 7, dtype=torch.int32, device=DEV)
+        ctx.rx_chunk_flow_dev(b, d, n, 0, out, bins)
+        ptrs, lens = ptr_burst(b, golden.desc)
+        out_p = dev_results(n)
+        bins_p = torch.full((n,), 7, dtype=torch.int32, device=DEV)
+        ctx.rx_ptrs_flow_dev(ptrs, lens, n, out_p, bins_p)
+        torch.cuda.synchronize()
+    got = out.cpu().numpy().view(RESULT_DTYPE)
+    assert not compare_results(got, golden)
+    assert np.array_equal(out.cpu().numpy(), out_p.cpu().numpy())
+    gb = bins.cpu().numpy().view(np.uint32)
+    ok = golden.meta["ref_ub"] == 0
+    assert np.array_equal(gb[ok], golden.flow_bins[ok])
+    assert np.array_equal(gb, oracle.flow_bins(got))
+    assert np.array_equal(bins_p.cpu().numpy().view(np.uint32), gb)
+
+
+@pytest.mark.parametrize("size,n", [(1500, 1 << 20), ("bimodal", (1 << 20) + 77), (1500, 3000)])
+def test_fused_flow_bins_equal_separate_pass(gpu, size, n):
+    """At full size (and past one launch's held passes) the fused bins equal
+    f3's separate kernel over the same records."""
+    seed = 63
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    d = to_dev(desc)
+    gpu.pktgen_dev(b, d, n, 6, seed)
+    out = dev_results(n)
+    bins = torch.full((n,), 7, dtype=torch.int32, device=DEV)
+    sep = torch.full((n,), 9, dtype=torch.int32, device=DEV)
+    out2 = dev_results(n)
+    with gpu.Context(0, rss=size == "bimodal", rss_queues=8) as ctx:
+        ctx.rx_chunk_flow_dev(b, d, n, 6, out, bins)
+        ctx.rx_chunk_dev(b, d, n, 6, out2)
+        ctx.flow_hash_dev(out, n, sep)
+        torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    assert torch.equal(bins, sep)
+    assert (bins.cpu().numpy().view(np.uint32) != 0xFFFFFFFF).mean() > 0.99
+
+
+def test_tx_fill_ptrs_golden(gpu, golden):
+    """mtcp_gpu_tx_fill_ptrs (host frames, e.g. a DPDK m_table burst) and
+    _dev (device-accessible frames): exactly the reference's fills, and only
+    the two check fields of the filled frames change."""
+    n = len(golden.desc)
+    offs = golden.desc["offset"].astype(np.int64)
+    want = golden.buf.copy()
+    assert oracle.tx_fill(want, golden.desc, 0) == golden.manifest["tx_filled"]
+    with gpu.Context(0) as ctx:
+        host = golden.buf.copy()
+        assert ctx.tx_fill_ptrs(host, offs, golden.desc["len"]) == golden.manifest["tx_filled"]
+        assert np.array_equal(host, want)
+        # a 64-frame burst (MAX_PKT_BURST) at 2-byte-aligned starts
+        buf2, d2 = repack(golden.buf, golden.desc[:64], 0, _even_phase)
+        w2 = buf2.copy()
+        k = oracle.tx_fill(w2, d2, 0)
+        h2 = buf2.copy()
+        assert ctx.tx_fill_ptrs(h2, d2["offset"].astype(np.int64), d2["len"]) == k
+        assert np.array_equal(h2, w2)
+        b = to_dev(golden.buf)
+        ptrs, lens = ptr_burst(b, golden.desc)
+        ctx.tx_fill_ptrs_dev(ptrs, lens, n)
+        torch.cuda.synchronize()
+        assert np.array_equal(b.cpu().numpy(), want)
+
+
+def test_reserve_and_rxq_after_host_calls(gpu, golden):
+    """mtcp_gpu_reserve(ctx, 0, 0) — which mtcp_gpu_rxq_create
+    calls — on a context whose stage 0 a host call already allocated."""
+    from mtcp_amd._lib import lib
+    L = lib()
+    with gpu.Context(0, rss=True, rss_queues=golden.rss_num_queues) as ctx:
+        got = ctx.rx_chunk(golden.buf, golden.desc, 0)           # allocates stage 0
+        assert not compare_results(got, golden)
+        ctx.reserve(0, 0)
+        q = ctypes.c_void_p()
+        assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 64, 64 * 2048) == 0
+        L.mtcp_gpu_rxq_destroy(q)
+        ctx.reserve(4096, 64)
+        ctx.reserve(0, 0)
+        got = ctx.rx_chunk(golden.buf, golden.desc, 0)
+        assert not compare_results(got, golden)

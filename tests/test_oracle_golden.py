@@ -124,6 +124,34 @@ def test_tx_fill_matches_reference(golden):
         assert buf[off + t + 16:off + t + 18].view("<u2")[0] == tx["tcp_check"][i]
 
 
+def _phase_even(i):            # every even start inside a 128 B line, odd ones rare
+    return (2 * i) % 128
+
+
+def test_rx_and_tx_at_every_even_start_match_reference(golden):
+    """The golden frames moved to every even start inside a 128 B line (2-byte
+    aligned starts: NET_IP_ALIGN-style buffers): the oracle's records equal
+    the reference's, and its tx fills write the reference's check values."""
+    from tests.repack import repack
+    buf, desc = repack(golden.buf, golden.desc, 0, _phase_even)
+    assert set((desc["offset"] % 4).tolist()) == {0, 2}
+    rss = oracle.rss_cfg(oracle.KEY_0X05, golden.rss_num_queues, 1)
+    got = oracle.rx_chunk(buf, desc, 0, rss)
+    bad = compare_results(got, golden)
+    assert not bad, bad
+    n = oracle.tx_fill(buf, desc, 0)
+    assert n == golden.manifest["tx_filled"]
+    tx = golden.tx
+    for i in np.nonzero(tx["filled"])[0]:
+        off, t = int(desc["offset"][i]), int(tx["T"][i])
+        assert buf[off + 24:off + 26].view("<u2")[0] == tx["ip_check"][i]
+        assert buf[off + t + 16:off + t + 18].view("<u2")[0] == tx["tcp_check"][i]
+    # an odd start is refused (BAD_DESC), as the ABI says
+    d = desc[:4].copy()
+    d["offset"] += 1
+    assert (oracle.rx_chunk(buf, d, 0)["verdict"] == 11).all()
+
+
 def test_pktgen_samples_match_fixture(golden):
     """The oracle's generator reproduces the sample bytes stored in the fixture."""
     for s in golden.manifest["samples"]:

@@ -30,6 +30,8 @@ for c in cfgs:
     s = json.load(open(summ))
     json.dump({
         "config": c,
+        # bench.py uses the figure only on this same build (bench.lib_sha256)
+        "lib_sha256": open(os.path.join(src, "lib.sha256")).read().strip(),
         "hbm_bytes_per_launch": s["hbm_bytes_per_launch"],
         "hbm_read_bytes_per_launch": s["hbm_read_bytes_per_launch"],
         "hbm_write_bytes_per_launch": s["hbm_write_bytes_per_launch"],
