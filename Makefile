@@ -7,7 +7,7 @@ ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
 LIB      := mtcp_amd/lib/libmtcp_gpu.so
 SRCS     := mtcp_amd/csrc/mtcp_gpu.hip mtcp_amd/csrc/pktgen.hip mtcp_amd/csrc/rxq.hip
-DEPS     := $(SRCS) mtcp_amd/csrc/rx_kernels.hpp mtcp_amd/csrc/host_copy.hpp mtcp_amd/csrc/flow_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h include/mtcp_gpu_rxq.h
+DEPS     := $(SRCS) mtcp_amd/csrc/rx_kernels.hpp mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/host_copy.hpp mtcp_amd/csrc/flow_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h include/mtcp_gpu_rxq.h
 
 .PHONY: all lib oracle ref golden examples clean tools
 
@@ -44,10 +44,13 @@ tools/store_probe: tools/store_probe.hip
 tools/pcie_probe: tools/pcie_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -w -o $@ $<
 
-tools: tools/rx_variants tools/hbm_ceiling tools/store_probe tools/pcie_probe
+tools: tools/rx_variants tools/hbm_ceiling tools/store_probe tools/pcie_probe tools/wave_probe
 
 # gpu_module.c driven by the RunMainLoop rx harness; the
 # mTCP types come from the test doubles in tests/c/mtcp_double.
 tests/c/rxloop: tests/c/rxloop.c mtcp_amd/io_module/gpu_module.c include/mtcp_gpu_rxq.h $(LIB)
 	gcc -std=gnu99 -O2 -Wall -pthread -Itests/c/mtcp_double -Iinclude -o $@ tests/c/rxloop.c \
 	    mtcp_amd/io_module/gpu_module.c -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib'
+
+tools/wave_probe: tools/wave_probe.hip mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/rx_kernels.hpp $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'

@@ -44,7 +44,7 @@ struct mtcp_gpu_ctx {
     uint32_t rss_nq = 1;
     uint32_t rss_endian = 0;
     uint32_t rss_key_w[4] = {0, 0, 0, 0};        // key bytes 0..15, big-endian words
-    uint32_t wave_upto = 0;                      // rx_wave_kernel for batches of <= this many
+    int sched = 0;                               // Sched: kSchedAuto unless MTCP_GPU_SCHED forces one
     hipStream_t stream = nullptr;
     uint32_t *d_rss_tables = nullptr;
     uint32_t *d_count = nullptr;
@@ -189,28 +189,73 @@ void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, 
 // cut into launches of at most grid x 4 waves x 64 x kHeldPasses packets.
 constexpr uint32_t kHeldPasses = 8;
 
-// One wavefront per packet (rx_wave.hpp) for small batches: rx_kernel gives
-// a wave 64 packets, so a batch of n packets runs on n/64 waves and its
-// phase 1 is a chain of round trips; the wave kernel puts n waves in flight.
-// Measured crossover: see DESIGN.md §4 (MTCP_GPU_WAVE_UPTO overrides it at
-// context open, for A/B runs and the parity tests of both schedules).
-constexpr uint32_t kWaveUpToPkts = 1u << 15;
+// Small batches (rx_wave.hpp).  rx_kernel gives a wave 64 packets, so a
+// batch of n packets runs on n/64 waves and its phase 1 is a chain of round
+// trips; the small-batch kernels put a wave (or a 16-lane row, or a 4-lane
+// quad) on every packet.  The choice by batch size and average slot, from
+// tools/wave_probe.hip and tools/small_batch_probe.py (same frames, same
+// process):
+//   n <= 4 096                       one wavefront per packet
+//   slot > 4 KiB, n <= 64 K          one wavefront per packet (a jumbo frame in one trip)
+//   slot < 256 B, n <= 64 K          a quad per packet, 256 packets per workgroup
+//   n <= 32 K                        a row per packet, 64 packets per workgroup
+//   otherwise                        rx_kernel (64 packets per wave)
+// Pointer bursts carry no size the host can see: they count as mid-size.
+// MTCP_GPU_SCHED=wave|row|quad|big at context open forces one kernel for
+// every batch (A/B runs, and the parity tests of each); the tx fill of
+// pointer bursts and the tx report exist only in the small kernels.
+enum Sched : int { kSchedAuto = 0, kSchedWave, kSchedRow, kSchedQuad, kSchedBig };
+
+int sched_from_env() {
+    const char *e = getenv("MTCP_GPU_SCHED");
+    if (!e) return kSchedAuto;
+    if (!strcmp(e, "wave")) return kSchedWave;
+    if (!strcmp(e, "row")) return kSchedRow;
+    if (!strcmp(e, "quad")) return kSchedQuad;
+    if (!strcmp(e, "big")) return kSchedBig;
+    return kSchedAuto;
+}
+
+int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_only) {
+    int s = ctx->sched;
+    if (s == kSchedAuto) {
+        if (n <= 4096) s = kSchedWave;
+        else if (slot > 4096) s = n <= (1u << 16) ? kSchedWave : kSchedBig;
+        else if (slot < 256) s = n <= (1u << 16) ? kSchedQuad : kSchedBig;
+        else s = n <= (1u << 15) ? kSchedRow : kSchedBig;
+    }
+    if (s == kSchedBig && small_only) s = kSchedRow;
+    return s;
+}
 
 template <int MODE, bool RSS>
-void launch_wave(uint32_t n, hipStream_t st, const mg::KParams &kp) {
-    hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS>), dim3((n + mg::kWavesPerBlock - 1) / mg::kWavesPerBlock),
-                       dim3(mg::kBlock), 0, st, kp);
+void launch_small(int sched, uint32_t n, hipStream_t st, const mg::KParams &kp) {
+    if (sched == kSchedWave) {
+        hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS>), dim3((n + mg::kWavesPerBlock - 1) / mg::kWavesPerBlock),
+                           dim3(mg::kBlock), 0, st, kp);
+    } else if (sched == kSchedQuad) {
+        constexpr uint32_t P = mg::GroupShape<4>::P;
+        hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 4>), dim3((n + P - 1) / P), dim3(mg::kGroupBlock), 0,
+                           st, kp);
+    } else {
+        constexpr uint32_t P = mg::GroupShape<16>::P;
+        hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 16>), dim3((n + P - 1) / P), dim3(mg::kGroupBlock), 0,
+                           st, kp);
+    }
 }
 
 template <int MODE>
 int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     if (kp.n == 0) return MTCP_GPU_OK;
     const bool rss = !mg::is_tx(MODE) && (ctx->flags & MTCP_GPU_F_RSS);
-    if (MODE == mg::kTxPtrs || kp.tx_report || kp.n <= ctx->wave_upto) {
+    const bool ptrs = MODE == mg::kRxPtrs || MODE == mg::kTxPtrs;
+    const int sched = pick_sched(ctx, kp.n, ptrs ? 1024 : kp.buf_len / kp.n,
+                                 MODE == mg::kTxPtrs || kp.tx_report != nullptr);
+    if (sched != kSchedBig) {
         if (rss)
-            launch_wave<MODE, true>(kp.n, st, kp);
+            launch_small<MODE, true>(sched, kp.n, st, kp);
         else
-            launch_wave<MODE, false>(kp.n, st, kp);
+            launch_small<MODE, false>(sched, kp.n, st, kp);
         return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
     }
     if constexpr (MODE != mg::kTxPtrs) {
@@ -335,8 +380,7 @@ int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rs
     for (int i = 0; i < 4; ++i)
         ctx->rss_key_w[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) |
                             ((uint32_t)key[4 * i + 2] << 8) | (uint32_t)key[4 * i + 3];
-    ctx->wave_upto = kWaveUpToPkts;
-    if (const char *e = getenv("MTCP_GPU_WAVE_UPTO")) ctx->wave_upto = (uint32_t)strtoul(e, nullptr, 10);
+    ctx->sched = sched_from_env();
     int rc = MTCP_GPU_OK;
     if (!HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) ||
         !HIP_OK(hipMalloc(&ctx->d_rss_tables, sizeof(tables))) ||

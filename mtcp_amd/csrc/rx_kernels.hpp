@@ -204,13 +204,132 @@ struct Pkt {
     uint32_t saddr = 0, daddr = 0, ports = 0, seq = 0, ack = 0, window = 0, flags = 0;
     uint32_t payload_len = 0;
     uint32_t T = 0, s_ip = 0, ip_check = 0;
+    uint32_t seg_len = 0;     // bytes of the summed segment [T, 14 + ip_len) (pseudo header length)
+    uint32_t tcheck = 0;      // tcph->check as received (tx: the sum is taken with it zeroed)
     bool tcp_entry = false;   // reached the TCP header: the 4-tuple is valid (RSS)
-    bool need_sum = false;    // the segment sum was taken (tx: fill this frame)
+    bool need_sum = false;    // the segment sum is needed (tx: fill this frame)
+    bool icmp = false;        // the segment is an ICMP message (no pseudo header)
 };
 
-// Phase 2 of one packet: the reference's rx chain in its order (eth_in.c:9-56,
-// ip_in.c:15-62, tcp_in.c:1138-1175), ip_fast_csum from the header words and
-// the TCP (or ICMP) checksum from the frame's chunk sum.
+// The reference's rx chain in its order (eth_in.c:9-56, ip_in.c:15-62, head
+// of tcp_in.c:1138-1175) up to the segment sum: verdict, fields, ip_fast_csum
+// from the header words, and whether and over which bytes the TCP (or ICMP)
+// checksum is taken.  pd(i) = packet dword i (bytes 4i..4i+3), read only for
+// the bytes each step has checked to lie inside the frame (L bytes);
+// ipsum(ihl) = the sum of the 16-bit words of the IP header, bytes
+// [14, 14 + 4*ihl), for 5 <= ihl <= 15 (ip_fast_csum's adc chain, exact:
+// SURVEY §8 a2').
+template <int MODE, class PD, class IPSUM>
+__device__ __forceinline__ Pkt parse_head(PD pd, IPSUM ipsum, uint32_t L, bool desc_ok) {
+    Pkt k;
+    uint32_t h[9];
+#pragma unroll
+    for (int i = 3; i < 9; ++i) h[i] = pd(i);
+    const uint32_t d0 = h[3];                 // bytes 12..15
+    if (!desc_ok) return k;
+    k.verdict = MTCP_GPU_V_TRUNCATED;
+    if (L < 14) return k;
+    k.eth_type = bswap16(d0 & 0xFFFFu);                                    // eth_in.c:13
+    if (k.eth_type != 0x0800u) {
+        k.verdict = k.eth_type == 0x0806u ? MTCP_GPU_V_ARP : MTCP_GPU_V_ETH_OTHER;
+        return k;
+    }
+    if (L < 18) return k;
+    k.ip_len = bswap16(h[4] & 0xFFFFu);                                    // ip_in.c:21
+    const uint32_t ihl = (d0 >> 16) & 0xFu;
+    k.ihl_doff = ihl;
+    const uint32_t ver = (d0 >> 20) & 0xFu;
+    if (!is_tx(MODE) && k.ip_len < 20) {
+        k.verdict = MTCP_GPU_V_IP_SHORT;                                   // ip_in.c:25-26
+        return k;
+    }
+    if (L < 14 + 4 * (ihl > 1 ? ihl : 1)) return k;
+    // ip_fast_csum: ihl <= 4 returns dword 0 as is (ps.h:72-73)
+    if (ihl >= 5) k.s_ip = ipsum(ihl);
+    k.ip_check = h[6] & 0xFFFFu;
+    k.ip_csum = ihl <= 4 ? (d0 >> 16) : fold_csum(k.s_ip);
+    const uint32_t proto = h[5] >> 24;                                     // ip_in.c:52
+    k.T = 14 + 4 * ihl;
+    bool tcp_entry = false;
+    if (is_tx(MODE)) {
+        tcp_entry = ver == 4 && ihl >= 5 && proto == 6 && L >= k.T + 20;
+        k.verdict = MTCP_GPU_V_ETH_OTHER;
+    } else if (k.ip_csum != 0) {
+        k.verdict = MTCP_GPU_V_IP_CSUM_BAD;                                // ip_in.c:35-36
+    } else if (ver != 4) {
+        k.verdict = MTCP_GPU_V_IP_VERSION;                                 // ip_in.c:47-50
+    } else if (proto == 1) {
+        k.verdict = MTCP_GPU_V_ICMP;
+        // ICMPChecksum(icmph, ip_len - 4*ihl) (icmp.c:18-42), the echo-request
+        // check of icmp.c:94, when the datagram lies inside the frame; a
+        // negative length skips the loop: ~0
+        if (14 + k.ip_len <= L) {
+            if (k.ip_len >= 4 * ihl) {
+                k.icmp = k.need_sum = true;
+                k.seg_len = k.payload_len = k.ip_len - 4 * ihl;
+            } else {
+                k.tcp_csum = 0xFFFFu;
+            }
+        }
+    } else if (proto != 6) {
+        k.verdict = MTCP_GPU_V_IP_PROTO_OTHER;                             // ip_in.c:57-59
+    } else if (L >= k.T + 16) {
+        tcp_entry = true;
+    }
+    if (tcp_entry) {
+        // tcp_in.c:1142-1149: tcph = iph + 4*ihl
+        const uint32_t tw = (k.T - 2) >> 2;
+        const uint32_t e0 = pd(tw), e1 = pd(tw + 1), e2 = pd(tw + 2);
+        const uint32_t e3 = pd(tw + 3), e4 = pd(tw + 4);
+        const uint32_t doff = (e3 >> 20) & 0xFu;
+        k.tcp_entry = true;
+        k.saddr = (h[6] >> 16) | (h[7] << 16);
+        k.daddr = (h[7] >> 16) | (h[8] << 16);
+        k.ports = (e0 >> 16) | (e1 << 16);                                 // sport | dport << 16
+        k.seq = bswap32((e1 >> 16) | (e2 << 16));
+        k.ack = bswap32((e2 >> 16) | (e3 << 16));
+        k.window = bswap16(e4 & 0xFFFFu);
+        k.flags = e3 >> 24;
+        k.tcheck = e4 >> 16;
+        k.ihl_doff = ihl | (doff << 4);
+        if (is_tx(MODE)) {
+            if (doff >= 5 && k.ip_len >= 4 * (ihl + doff) && 14 + k.ip_len <= L) {
+                k.need_sum = true;
+                k.seg_len = k.ip_len - 4 * ihl;
+            }
+        } else if (k.ip_len < ((ihl + doff) << 2)) {
+            k.verdict = MTCP_GPU_V_TCP_LEN_BAD;                            // tcp_in.c:1155-1156
+        } else {
+            k.payload_len = k.ip_len - ((ihl + doff) << 2);                // tcp_in.c:1144
+            if (14 + k.ip_len <= L) {
+                k.need_sum = true;
+                k.seg_len = k.ip_len - 4 * ihl;                            // tcp_in.c:1166
+            }
+        }
+    }
+    return k;
+}
+
+// The checksum from the exact word sum of the segment [T, 14 + ip_len):
+// TCPCalcChecksum's pseudo header and two-step fold (tcp_util.c:157-190),
+// or ICMPChecksum's fold (icmp.c:36-38); the rx verdict (tcp_in.c:1167-1173).
+template <int MODE>
+__device__ __forceinline__ void finish_seg(Pkt &k, uint32_t seg) {
+    uint32_t s = seg;
+    if (is_tx(MODE)) s -= k.tcheck;                            // computed with check = 0
+    if (!k.icmp) {
+        s += (k.saddr & 0xFFFFu) + (k.saddr >> 16);            // tcp_util.c:179-182
+        s += (k.daddr & 0xFFFFu) + (k.daddr >> 16);
+        s += bswap16(k.seg_len);
+        s += 0x0600u;                                          // htons(IPPROTO_TCP)
+    }
+    k.tcp_csum = fold_csum(s);
+    if (!is_tx(MODE) && !k.icmp)
+        k.verdict = k.tcp_csum ? MTCP_GPU_V_TCP_CSUM_BAD : MTCP_GPU_V_TCP_OK;
+}
+
+// Phase 2 of one packet from the LDS copy of its header chunks and its
+// chunk sum (rx_kernel's per-lane phase 2):
 //   raw[i * S], i < 28: dword i of the frame's first seven 16 B chunks on the
 //                       absolute grid (chunk 0 holds the frame's first byte);
 //   raw[(28 + j) * S]:  dword j of its last chunk;
@@ -218,114 +337,28 @@ struct Pkt {
 // The frame starts at any even address p (sh = p & 15 bytes into chunk 0):
 // packet dword i is the funnel of raw dwords a+i and a+i+1 (a = sh / 4) by
 // 8 * (sh & 3) bits, and each 16-bit word of the packet is still a whole
-// half of one aligned dword, which keeps the sum exact.
-// BULK (the wave kernel, wave-uniform operands): the header dwords that the
-// subtraction needs are read from LDS in one batch instead of one
-// conditional read per dword, each of which would wait out the LDS latency.
+// half of one aligned dword, which keeps the sum exact.  The segment sum is
+// the chunk sum minus the bytes outside [T, 14 + ip_len).
+// BULK: the header dwords that the subtraction needs are read from LDS in one
+// batch instead of one conditional read per dword.
 template <int MODE, int S, bool BULK = false>
 __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, uint64_t p,
                                             uint32_t L, uint32_t nch, bool desc_ok) {
-    Pkt k;
     const uint32_t sh = (uint32_t)(p & 15);
     const uint32_t a = sh >> 2, fb = 8 * (sh & 3);
     auto pd = [&](uint32_t i) -> uint32_t {      // packet dword i (bytes 4i..4i+3)
         return __builtin_amdgcn_alignbit(raw[(a + i + 1) * S], raw[(a + i) * S], fb);
     };
-    uint32_t h[19];
+    auto ipsum = [&](uint32_t ihl) -> uint32_t {  // words [14, 14 + 4*ihl): dwords 3..3+ihl
+        uint32_t s_ip = pd(3) >> 16, lo_last = 0;
 #pragma unroll
-    for (int i = 3; i < 19; ++i) h[i] = pd(i);
-    const uint32_t d0 = h[3];                 // bytes 12..15
-    uint32_t tcp_len = 0, tcheck = 0;
-    bool icmp = false;
-    if (desc_ok) {
-        k.verdict = MTCP_GPU_V_TRUNCATED;
-        if (L >= 14) {
-            k.eth_type = bswap16(d0 & 0xFFFFu);                            // eth_in.c:13
-            if (k.eth_type != 0x0800u) {
-                k.verdict = k.eth_type == 0x0806u ? MTCP_GPU_V_ARP : MTCP_GPU_V_ETH_OTHER;
-            } else if (L >= 18) {
-                k.ip_len = bswap16(h[4] & 0xFFFFu);                        // ip_in.c:21
-                const uint32_t ihl = (d0 >> 16) & 0xFu;
-                k.ihl_doff = ihl;
-                const uint32_t ver = (d0 >> 20) & 0xFu;
-                if (!is_tx(MODE) && k.ip_len < 20) {
-                    k.verdict = MTCP_GPU_V_IP_SHORT;                       // ip_in.c:25-26
-                } else if (L >= 14 + 4 * (ihl > 1 ? ihl : 1)) {
-                    // ip_fast_csum: ihl <= 4 returns dword 0 as is (ps.h:72-73)
-                    uint32_t s_ip = d0 >> 16, lo_last = 0;
-#pragma unroll
-                    for (int j = 1; j < 16; ++j) {
-                        if (j < (int)ihl) s_ip = halves(h[3 + j], s_ip);
-                        if (j == (int)ihl) lo_last = h[3 + j] & 0xFFFFu;
-                    }
-                    s_ip += lo_last;
-                    k.s_ip = s_ip;
-                    k.ip_check = h[6] & 0xFFFFu;
-                    k.ip_csum = ihl <= 4 ? (d0 >> 16) : fold_csum(s_ip);
-                    const uint32_t proto = h[5] >> 24;                     // ip_in.c:52
-                    k.T = 14 + 4 * ihl;
-                    bool tcp_entry = false;
-                    if (is_tx(MODE)) {
-                        tcp_entry = ver == 4 && ihl >= 5 && proto == 6 && L >= k.T + 20;
-                        k.verdict = MTCP_GPU_V_ETH_OTHER;
-                    } else if (k.ip_csum != 0) {
-                        k.verdict = MTCP_GPU_V_IP_CSUM_BAD;                // ip_in.c:35-36
-                    } else if (ver != 4) {
-                        k.verdict = MTCP_GPU_V_IP_VERSION;                 // ip_in.c:47-50
-                    } else if (proto == 1) {
-                        k.verdict = MTCP_GPU_V_ICMP;
-                        // ICMPChecksum(icmph, ip_len - 4*ihl) (icmp.c:18-42), the
-                        // echo-request check of icmp.c:94, when the datagram lies
-                        // inside the frame; a negative length skips the loop: ~0
-                        if (14 + k.ip_len <= L) {
-                            if (k.ip_len >= 4 * ihl) {
-                                icmp = k.need_sum = true;
-                                tcp_len = k.payload_len = k.ip_len - 4 * ihl;
-                            } else {
-                                k.tcp_csum = 0xFFFFu;
-                            }
-                        }
-                    } else if (proto != 6) {
-                        k.verdict = MTCP_GPU_V_IP_PROTO_OTHER;             // ip_in.c:57-59
-                    } else if (L >= k.T + 16) {
-                        tcp_entry = true;
-                    }
-                    if (tcp_entry) {
-                        // tcp_in.c:1142-1149: tcph = iph + 4*ihl
-                        const uint32_t tw = (k.T - 2) >> 2;
-                        const uint32_t e0 = pd(tw), e1 = pd(tw + 1), e2 = pd(tw + 2);
-                        const uint32_t e3 = pd(tw + 3), e4 = pd(tw + 4);
-                        const uint32_t doff = (e3 >> 20) & 0xFu;
-                        k.tcp_entry = true;
-                        k.saddr = (h[6] >> 16) | (h[7] << 16);
-                        k.daddr = (h[7] >> 16) | (h[8] << 16);
-                        k.ports = (e0 >> 16) | (e1 << 16);                 // sport | dport << 16
-                        k.seq = bswap32((e1 >> 16) | (e2 << 16));
-                        k.ack = bswap32((e2 >> 16) | (e3 << 16));
-                        k.window = bswap16(e4 & 0xFFFFu);
-                        k.flags = e3 >> 24;
-                        tcheck = e4 >> 16;
-                        k.ihl_doff = ihl | (doff << 4);
-                        if (is_tx(MODE)) {
-                            if (doff >= 5 && k.ip_len >= 4 * (ihl + doff) && 14 + k.ip_len <= L) {
-                                k.need_sum = true;
-                                tcp_len = k.ip_len - 4 * ihl;
-                            }
-                        } else if (k.ip_len < ((ihl + doff) << 2)) {
-                            k.verdict = MTCP_GPU_V_TCP_LEN_BAD;            // tcp_in.c:1155-1156
-                        } else {
-                            k.payload_len = k.ip_len - ((ihl + doff) << 2);   // tcp_in.c:1144
-                            if (14 + k.ip_len <= L) {
-                                k.need_sum = true;
-                                tcp_len = k.ip_len - 4 * ihl;              // tcp_in.c:1166
-                            }
-                        }
-                    }
-                }
-            }
+        for (int j = 1; j < 16; ++j) {
+            if (j < (int)ihl) s_ip = halves(pd(3 + j), s_ip);
+            if (j == (int)ihl) lo_last = pd(3 + j) & 0xFFFFu;
         }
-    }
-
+        return s_ip + lo_last;
+    };
+    Pkt k = parse_head<MODE>(pd, ipsum, L, desc_ok);
     if (k.need_sum) {
         // The chunk sum covers [p16, p16 + 16*nch).  Remove the bytes before
         // the frame, the header bytes [0, T), and everything at or past
@@ -380,17 +413,7 @@ __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, u
             const uint4 w = gload4(cstart);
             s_out = halves(w.w, halves(w.z, halves(w.y, halves(w.x, s_out))));
         }
-        uint32_t s = sum - s_out;                                  // exact segment sum
-        if (is_tx(MODE)) s -= tcheck;                         // computed with check = 0
-        if (!icmp) {
-            s += (k.saddr & 0xFFFFu) + (k.saddr >> 16);            // tcp_util.c:179-182
-            s += (k.daddr & 0xFFFFu) + (k.daddr >> 16);
-            s += bswap16(tcp_len);
-            s += 0x0600u;                                          // htons(IPPROTO_TCP)
-        }
-        k.tcp_csum = fold_csum(s);                                 // icmp.c:36-38 folds alike
-        if (!is_tx(MODE) && !icmp)
-            k.verdict = k.tcp_csum ? MTCP_GPU_V_TCP_CSUM_BAD : MTCP_GPU_V_TCP_OK;   // tcp_in.c:1167-1173
+        finish_seg<MODE>(k, sum - s_out);                          // exact segment sum
     }
     return k;
 }
@@ -408,6 +431,24 @@ __device__ __forceinline__ void pack_record(const Pkt &k, uint32_t rss_hash, uin
     r[7] = rss_hash;
     r[8] = k.payload_len | (k.ihl_doff << 16) | (k.flags << 24);
     r[9] = k.verdict | (rss_queue << 8) | (k.eth_type << 16);
+}
+
+// util/rss.c:107-145 as 24 nibble tables (built on the host from the key
+// cache of BuildKeyCache, util/rss.c:13-105): the input bytes (sip, dip, sp,
+// dp host order, MSB first) are saddr / daddr / ports in memory order.
+__device__ __forceinline__ uint32_t toeplitz_tables(const uint32_t *tab, uint32_t saddr,
+                                                    uint32_t daddr, uint32_t ports) {
+    uint32_t hh = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t sb = (saddr >> (8 * b)) & 0xFFu;
+        const uint32_t db = (daddr >> (8 * b)) & 0xFFu;
+        const uint32_t pb = (ports >> (8 * b)) & 0xFFu;
+        hh ^= tab[((2 * b) << 4) | (sb >> 4)] ^ tab[((2 * b + 1) << 4) | (sb & 15)];
+        hh ^= tab[((8 + 2 * b) << 4) | (db >> 4)] ^ tab[((9 + 2 * b) << 4) | (db & 15)];
+        hh ^= tab[((16 + 2 * b) << 4) | (pb >> 4)] ^ tab[((17 + 2 * b) << 4) | (pb & 15)];
+    }
+    return hh;
 }
 
 // util/rss.c:153-165 / mtcp/src/rss.c:90-103: off[m & 3] = {3,1,-1,-3} == m ^ 3
@@ -999,21 +1040,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         uint32_t rss_hash = 0, rss_queue = 0;
         if constexpr (RSS) {
             if (pk.tcp_entry) {
-                // util/rss.c:107-145 as 24 nibble tables: the input bytes
-                // (sip, dip, sp, dp host order, MSB first) are saddr/daddr/ports
-                // in memory order.
-                uint32_t hh = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint32_t sb = (pk.saddr >> (8 * b)) & 0xFFu;
-                    const uint32_t db = (pk.daddr >> (8 * b)) & 0xFFu;
-                    const uint32_t pb = (pk.ports >> (8 * b)) & 0xFFu;
-                    hh ^= rss_lds[((2 * b) << 4) | (sb >> 4)] ^ rss_lds[((2 * b + 1) << 4) | (sb & 15)];
-                    hh ^= rss_lds[((8 + 2 * b) << 4) | (db >> 4)] ^ rss_lds[((9 + 2 * b) << 4) | (db & 15)];
-                    hh ^= rss_lds[((16 + 2 * b) << 4) | (pb >> 4)] ^ rss_lds[((17 + 2 * b) << 4) | (pb & 15)];
-                }
-                rss_hash = hh;
-                rss_queue = rss_core(hh, kp.rss_nq, kp.rss_endian);
+                rss_hash = toeplitz_tables(rss_lds, pk.saddr, pk.daddr, pk.ports);
+                rss_queue = rss_core(rss_hash, kp.rss_nq, kp.rss_endian);
             }
         }
 

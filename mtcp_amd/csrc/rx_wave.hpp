@@ -31,7 +31,7 @@
 
 namespace mg {
 
-constexpr int kWaveLoads = 8;   // 16 B loads per lane per trip: 8 KiB of frame
+constexpr int kWaveLoads = 10;  // 16 B loads per lane per trip: 10 KiB of frame (a 9000 B frame in one)
 
 // XOR over the 64 lanes (DPP row_shr steps, then the four row results).
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
@@ -59,16 +59,19 @@ __device__ __forceinline__ uint32_t toeplitz_wave(const uint32_t (&kw)[4], uint3
     return wave_xor(v);
 }
 
-template <int MODE, bool RSS>
+// ABL (profiling only, tools/wave_probe.hip): 1 = the frame stream and its
+// plain chunk sum only (lane 0 stores it); 2 = descriptor only (stores L).
+template <int MODE, bool RSS, int ABL = 0>
 __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
-    __shared__ uint4 lds[kWavesPerBlock][kSlotChunks];     // chunks 0..6, then the last chunk
+    __shared__ uint4 lds[kWavesPerBlock][kSlotChunks];     // the frame's chunks 0..6
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t k = blockIdx.x * kWavesPerBlock + wib;  // this wave's packet
     if (k >= kp.n) return;
-    uint4 *hd = lds[wib];
+    uint4 *hd4 = lds[wib];
+    const uint32_t *hd = reinterpret_cast<const uint32_t *>(hd4);
 
-    // ---- descriptor (wave-uniform) ------------------------------------------
+    // ---- descriptor (wave-uniform, scalar loads) ------------------------------------
     uint64_t p = 0;
     uint32_t L;
     bool ok;
@@ -86,11 +89,15 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
     }
     const uint64_t p16 = p & ~15ull;
     const uint32_t nch = ok && L ? (uint32_t)((((p + L + 15) & ~15ull) - p16) >> 4) : 0u;
+    if constexpr (ABL == 2) {
+        if (lane == 0) kp.out[k].saddr = L;
+        return;
+    }
 
-    // ---- phase 1: the whole wave streams the frame ----------------------------
-    uint32_t acc = 0;
-    for (uint32_t c0 = 0; c0 < nch; c0 += kWave * kWaveLoads) {
-        v4u x[kWaveLoads];
+    // ---- phase 1: the wave issues the frame's first trip (10 KiB) --------------------
+    constexpr uint32_t kTrip = kWave * kWaveLoads;
+    v4u x[kWaveLoads];
+    auto issue = [&](uint32_t c0) {
 #pragma unroll
         for (int u = 0; u < kWaveLoads; ++u) {
             if (c0 + u * kWave < nch) {                    // wave-uniform
@@ -98,26 +105,83 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
                 x[u] = gload_nt(p16 + 16ull * (c < nch ? c : nch - 1));
             }
         }
+    };
+    issue(0);
+    if constexpr (ABL == 1) {
+        uint32_t acc = 0;
+        for (uint32_t c0 = 0; c0 < nch; c0 += kTrip) {
+            if (c0) issue(c0);
 #pragma unroll
-        for (int u = 0; u < kWaveLoads; ++u) {
-            if (c0 + u * kWave < nch) {
+            for (int u = 0; u < kWaveLoads; ++u)
+                if (c0 + u * kWave < nch && c0 + u * kWave + lane < nch) acc = halves4(x[u], acc);
+        }
+        acc = row_sum(acc);
+        const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)acc, 15) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 31) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 47) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 63);
+        if (lane == 0) kp.out[k].saddr = sum;
+        return;
+    }
+
+    // ---- phase 2a: the header, as soon as chunks 0..6 arrive (lanes 0..6 of
+    //      the first load).  Lane i then holds packet dword i (i < 25, funneled
+    //      for 2-byte-aligned starts); the fields are readlanes of it, the IP
+    //      header sum a 32-lane reduction, the verdict chain scalar code. ----------
+    if (nch && lane < kSlotChunks - 1) hd4[lane] = make_uint4(x[0].x, x[0].y, x[0].z, x[0].w);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t sh = (uint32_t)(p & 15);
+    const uint32_t a = sh >> 2, fb = 8 * (sh & 3);
+    const uint32_t li = lane < 25 ? lane : 24u;
+    const uint32_t pdw = __builtin_amdgcn_alignbit(hd[a + li + 1], hd[a + li], fb);
+    auto pd = [&](uint32_t i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)pdw, (int)i); };
+    auto ipsum = [&](uint32_t ihl) -> uint32_t {
+        // words of bytes [14, 14 + 4*ihl): the high half of dword 3, dwords
+        // 4 .. 2 + ihl, the low half of dword 3 + ihl
+        const uint32_t w = lane == 3 ? pdw >> 16
+                           : lane > 3 && lane < 3 + ihl ? (pdw & 0xFFFFu) + (pdw >> 16)
+                           : lane == 3 + ihl ? pdw & 0xFFFFu : 0u;
+        const uint32_t r = row_sum(w);
+        return (uint32_t)__builtin_amdgcn_readlane((int)r, 15) + (uint32_t)__builtin_amdgcn_readlane((int)r, 31);
+    };
+    Pkt pk = parse_head<MODE>(pd, ipsum, L, ok);
+
+    // ---- phase 2b: the segment [T, 14 + ip_len), summed by the lanes holding it --------
+    if (pk.need_sum) {
+        const uint32_t lo = sh + pk.T, span = 14 + pk.ip_len - pk.T;   // bytes [lo, lo + span) of the grid
+        uint32_t acc = 0;
+        auto take = [&](const v4u &v, uint32_t c) {
+            const uint32_t cb = 16 * c - lo;                // chunk start relative to the segment
+            if (cb <= span - 16 && span >= 16) {            // whole chunk inside
+                acc = halves4(v, acc);
+            } else if (16 * c < lo + span && 16 * c + 16 > lo) {
+                // a boundary chunk: keep its bytes inside the segment (an odd
+                // span ends on the low byte of a word: tcp_util.c:176)
+                const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t o = cb + 4 * j;          // wraps below the segment
+                    const uint32_t m = (o < span ? 0xFFu : 0u) | (o + 1 < span ? 0xFF00u : 0u) |
+                                       (o + 2 < span ? 0xFF0000u : 0u) | (o + 3 < span ? 0xFF000000u : 0u);
+                    acc = halves(d[j] & m, acc);
+                }
+            }
+        };
+        for (uint32_t c0 = 0; c0 < nch; c0 += kTrip) {
+            if (c0) issue(c0);                              // jumbo frames: later trips
+#pragma unroll
+            for (int u = 0; u < kWaveLoads; ++u) {
                 const uint32_t c = c0 + u * kWave + lane;
-                if (c < nch) acc = halves4(x[u], acc);
-                const uint4 v = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
-                if (u == 0 && c < kSlotChunks - 1) hd[c] = v;          // raw chunks 0..6
-                if (c == nch - 1) hd[kSlotChunks - 1] = v;             // last chunk
+                if (c0 + u * kWave < nch && c < nch) take(x[u], c);
             }
         }
+        acc = row_sum(acc);
+        const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)acc, 15) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 31) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 47) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 63);
+        finish_seg<MODE>(pk, seg);
     }
-    acc = row_sum(acc);
-    const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)acc, 15) +
-                         (uint32_t)__builtin_amdgcn_readlane((int)acc, 31) +
-                         (uint32_t)__builtin_amdgcn_readlane((int)acc, 47) +
-                         (uint32_t)__builtin_amdgcn_readlane((int)acc, 63);
-    __builtin_amdgcn_wave_barrier();
-
-    // ---- phase 2: parse and finish, wave-uniform -------------------------------
-    const Pkt pk = parse_finish<MODE, 1, true>(reinterpret_cast<const uint32_t *>(hd), sum, p, L, nch, ok);
 
     if constexpr (is_tx(MODE)) {
         if (lane == 0) {
@@ -144,13 +208,165 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
         uint32_t r[10];
         pack_record(pk, rss_hash, rss_queue, r);
         if (lane < 5) {
-            uint32_t x = r[0], y = r[1];
+            uint32_t xx = r[0], yy = r[1];
 #pragma unroll
             for (int i = 1; i < 5; ++i)
-                if (lane == (uint32_t)i) x = r[2 * i], y = r[2 * i + 1];
-            reinterpret_cast<uint2 *>(kp.out + k)[lane] = make_uint2(x, y);
+                if (lane == (uint32_t)i) xx = r[2 * i], yy = r[2 * i + 1];
+            reinterpret_cast<uint2 *>(kp.out + k)[lane] = make_uint2(xx, yy);
         }
         if (kp.bins && lane == 0) kp.bins[k] = flow_bin(r[0], r[1], r[2], r[9] & 0xFFu);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The small-batch kernel as dispatched: phase 1 with G lanes per packet (a
+// whole wave per packet for G = 64, the north star's shape; a 16-lane row or
+// a 4-lane quad for smaller frames), phase 2 with ONE LANE per packet.
+//
+// rx_wave_kernel above runs phase 2 on the whole wave with wave-uniform
+// operands, i.e. ~400 wave-instructions per packet: measured
+// (tools/wave_probe.hip) its phase 1 over 4 096 x 1500 B costs 2.6 us — the
+// launch floor, 2.5 us — and its phase 2 another 2.6 us, all VALU issue.  Here a
+// 16-wave workgroup streams P = 1024 / G packets, leaves each packet's chunk
+// sum, header chunks, last chunk and descriptor in LDS (packet-minor, as in
+// rx_kernel), meets at one barrier, and then P lanes parse P packets in one
+// instruction stream (parse_finish, the code rx_kernel runs), so phase 2
+// costs 1/P of the wave-uniform version's issue slots.
+constexpr int kGroupBlock = 1024;              // 16 waves
+
+template <int G>
+struct GroupShape {
+    static_assert(G == 4 || G == 16 || G == 64, "lanes per packet: a quad, a row or the wave");
+    static constexpr int P = kGroupBlock / G;                   // packets per workgroup
+    static constexpr int U = G == 64 ? 8 : G == 16 ? 6 : 2;     // loads per lane per trip
+    static constexpr int R = G >= 16 ? G / 16 : 1;              // partial sums per packet
+    static constexpr int S = P + 1;                             // LDS stride (odd: no conflicts)
+    static constexpr int W2 = (P + kWave - 1) / kWave;          // waves that run phase 2
+};
+
+// ABL (profiling only, tools/wave_probe.hip): 1 = phase 2 stores the sum only.
+template <int MODE, bool RSS, int G, int ABL = 0>
+__global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
+    using Sh = GroupShape<G>;
+    constexpr int P = Sh::P, U = Sh::U, R = Sh::R, S = Sh::S;
+    __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
+    __shared__ uint32_t hd[kHdRows * S];       // dword i of packet q at hd[i * S + q]
+    __shared__ uint32_t psum[P * R];
+    __shared__ uint4 info[P];                  // {p lo, p hi, L | ok << 16, nch}
+    if constexpr (RSS) {
+        for (int i = threadIdx.x; i < kRssTableWords; i += kGroupBlock) rss_lds[i] = kp.rss_tables[i];
+    }
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wib = threadIdx.x >> 6;
+    const uint32_t gl = lane % G;
+    const uint32_t pkt = wib * (kWave / G) + lane / G;     // packet within the workgroup
+    const uint32_t k = blockIdx.x * P + pkt;
+    constexpr bool kPtrs = MODE == kRxPtrs || MODE == kTxPtrs;
+    const uint64_t safe = (uint64_t)(uintptr_t)(kPtrs ? (const void *)kp.lens : (const void *)kp.buf);
+
+    // ---- descriptor -----------------------------------------------------------
+    uint64_t p = safe;
+    uint32_t L = 0;
+    bool ok = false;
+    if (k < kp.n) {
+        if constexpr (kPtrs) {
+            const uint64_t a = (uint64_t)(uintptr_t)kp.ptrs[k];
+            L = kp.lens[k];
+            ok = a != 0 && (a & 1) == 0;                   // any even start
+            if (ok) p = a;
+        } else {
+            const uint64_t raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
+            L = (uint32_t)(raw >> 32) & 0xFFFFu;
+            const int64_t pos = (int64_t)((uint64_t)(uint32_t)raw << kp.off_shift) - kp.base_sub;
+            ok = pos >= 0 && (pos & 1) == 0 && (uint64_t)pos + L <= kp.buf_len;
+            if (ok) p = safe + (uint64_t)pos;
+        }
+    }
+    const uint64_t p16 = p & ~15ull;
+    const uint32_t nch = ok && L ? (uint32_t)((((p + L + 15) & ~15ull) - p16) >> 4) : 0u;
+
+    // ---- phase 1: G lanes stream each frame -------------------------------------
+    uint32_t acc = 0;
+    for (uint32_t c0 = 0; __ballot(c0 < nch); c0 += U * G) {
+        v4u x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (__ballot(c0 + u * G < nch)) {              // some frame of the wave needs load u
+                const uint32_t c = c0 + u * G + gl;
+                const uint32_t cc = c < nch ? c : (nch ? nch - 1 : 0u);   // clamp: no exec mask
+                x[u] = gload_nt(p16 + 16ull * cc);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (__ballot(c0 + u * G < nch)) {
+                const uint32_t c = c0 + u * G + gl;
+                if (c < nch) {
+                    acc = halves4(x[u], acc);
+                    if (c < kSlotChunks - 1) {                      // raw chunks 0..6
+                        uint32_t *d = hd + 4 * c * S + pkt;
+                        d[0] = x[u].x; d[S] = x[u].y; d[2 * S] = x[u].z; d[3 * S] = x[u].w;
+                    }
+                    if (c == nch - 1) {                             // last chunk
+                        uint32_t *d = hd + 4 * (kSlotChunks - 1) * S + pkt;
+                        d[0] = x[u].x; d[S] = x[u].y; d[2 * S] = x[u].z; d[3 * S] = x[u].w;
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (G == 4) {
+        acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+        acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+        if (gl == 0) psum[pkt] = acc;
+    } else {
+        acc = row_sum(acc);
+        if ((lane & (kRow - 1)) == kRow - 1) psum[pkt * R + gl / kRow] = acc;
+    }
+    if (gl == 0) info[pkt] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), L | ((uint32_t)ok << 16), nch);
+    __syncthreads();
+
+    // ---- phase 2: one lane per packet --------------------------------------------
+    if (wib >= (uint32_t)Sh::W2) return;
+    const uint32_t q = wib * kWave + lane;
+    const uint32_t kk = blockIdx.x * P + q;
+    if (q >= (uint32_t)P || kk >= kp.n) return;
+    const uint4 inf = info[q];
+    const uint64_t pq = ((uint64_t)inf.y << 32) | inf.x;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) sum += psum[q * R + r];
+    if constexpr (ABL == 1) {
+        kp.out[kk].saddr = sum;
+        return;
+    }
+    const Pkt pk = parse_finish<MODE, S, true>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);
+    if constexpr (is_tx(MODE)) {
+        const uint32_t checks = fold_csum(pk.s_ip - pk.ip_check) | (pk.tcp_csum << 16);
+        if (kp.tx_report) {
+            // report mode (mtcp_gpu_tx_fill_ptrs): the host writes the two
+            // fields into its own frames; T = 0: not filled
+            kp.tx_report[kk] = make_uint2(pk.need_sum ? checks : 0u, pk.need_sum ? pk.T : 0u);
+        } else if (pk.need_sum) {
+            uint16_t *q16 = reinterpret_cast<uint16_t *>(pq);
+            q16[12] = (uint16_t)checks;                            // iph->check (ip_out.c:145,164)
+            q16[(pk.T + 16) >> 1] = (uint16_t)(checks >> 16);      // tcph->check (tcp_out.c:329)
+        }
+        if (pk.need_sum && kp.fill_count) atomicAdd(kp.fill_count, 1u);
+    } else {
+        uint32_t rss_hash = 0, rss_queue = 0;
+        if constexpr (RSS) {
+            if (pk.tcp_entry) {
+                rss_hash = toeplitz_tables(rss_lds, pk.saddr, pk.daddr, pk.ports);
+                rss_queue = rss_core(rss_hash, kp.rss_nq, kp.rss_endian);
+            }
+        }
+        uint32_t r[10];
+        pack_record(pk, rss_hash, rss_queue, r);
+        uint2 *o = reinterpret_cast<uint2 *>(kp.out + kk);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) o[i] = make_uint2(r[2 * i], r[2 * i + 1]);
+        if (kp.bins) kp.bins[kk] = flow_bin(r[0], r[1], r[2], r[9] & 0xFFu);
     }
 }
 

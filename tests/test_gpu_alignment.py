@@ -66,7 +66,7 @@ def _unaligned_batch(kind, n=1536, seed=11):
                                                     ("mid", 1024, 1536, 1536),
                                                     ("small", 0, 1023, 1536)])
 def test_unaligned_frames_every_schedule(gpu, kind, slot_lo, slot_hi, n, monkeypatch):
-    monkeypatch.setenv("MTCP_GPU_WAVE_UPTO", "0")      # rx_kernel's schedules (test_gpu_wave: the wave kernel)
+    monkeypatch.setenv("MTCP_GPU_SCHED", "big")        # rx_kernel's schedules (test_gpu_wave: the small kernels)
     buf, desc = _unaligned_batch(kind, n)
     padded = buf.nbytes + (-buf.nbytes) % 16
     assert slot_lo <= padded // len(desc) <= slot_hi        # the schedule under test is dispatched

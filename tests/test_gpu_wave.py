@@ -1,11 +1,12 @@
 """Small batches and the entry points added with the wave-per-packet kernel
 (mtcp_amd/csrc/rx_wave.hpp), on the MI355X, bit-exact:
 
-* every dispatched schedule — the wave kernel (batches of at most
-  kWaveUpToPkts packets, mtcp_gpu.hip) and rx_kernel's sorted / unrolled /
-  line-aligned rounds (forced with MTCP_GPU_WAVE_UPTO=0) — on the golden
-  vectors and on config-shaped batches of 4 096 (one io_module aggregate)
-  and 65 536 packets, against the reference's results and the oracle;
+* every dispatched kernel — a wavefront, a 16-lane row or a 4-lane quad per
+  packet (rx_wave.hpp) and rx_kernel's sorted / unrolled / line-aligned
+  rounds, each forced with MTCP_GPU_SCHED (mtcp_gpu.hip pick_sched) — on the
+  golden vectors and on config-shaped batches of 4 096 (one io_module
+  aggregate) and 65 536 packets, against the reference's results and the
+  oracle;
 * frames at every even start (2-byte aligned, NET_IP_ALIGN-style), chunk and
   pointer modes, rx and tx;
 * rx with HashFlow fused in (mtcp_gpu_rx_*_flow_dev) against the reference's
@@ -29,9 +30,6 @@ from tests.test_gpu_parity import DEV, assert_same, dev_results, run_rx_dev, to_
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-WAVE_UPTO = 1 << 15          # mtcp_gpu.hip kWaveUpToPkts
-
-
 @pytest.fixture(scope="module")
 def gpu():
     if not torch.cuda.is_available():
@@ -41,11 +39,11 @@ def gpu():
 
 
 def ctx_for(gpu, monkeypatch, sched, **kw):
-    """A context whose small batches take `sched`: "wave" (every batch size) or
-    "rows" (rx_kernel's schedules only)."""
-    monkeypatch.setenv("MTCP_GPU_WAVE_UPTO", str(1 << 31) if sched == "wave" else "0")
+    """A context whose batches all take kernel `sched` (mtcp_gpu.hip
+    MTCP_GPU_SCHED): "wave", "row", "quad" (rx_wave.hpp) or "big" (rx_kernel)."""
+    monkeypatch.setenv("MTCP_GPU_SCHED", sched)
     c = gpu.Context(0, **kw)
-    monkeypatch.delenv("MTCP_GPU_WAVE_UPTO")
+    monkeypatch.delenv("MTCP_GPU_SCHED")
     return c
 
 
@@ -55,7 +53,7 @@ def ptr_burst(b, desc):
     return ptrs, lens
 
 
-SCHEDS = ["wave", "rows"]
+SCHEDS = ["wave", "row", "quad", "big"]
 
 
 @pytest.mark.parametrize("sched", SCHEDS)
@@ -88,8 +86,8 @@ def test_golden_every_schedule(gpu, golden, monkeypatch, sched):
 @pytest.mark.parametrize("n", [4096, 1 << 16])
 @pytest.mark.parametrize("size,rss", [(1500, False), ("bimodal", True), (64, False), (9000, False)])
 def test_small_batches_every_schedule(gpu, monkeypatch, n, size, rss):
-    """One io_module aggregate (4 096 frames) and 64 K frames: the wave kernel
-    and rx_kernel's schedule for the same batch, both equal to the oracle."""
+    """One io_module aggregate (4 096 frames) and 64 K frames through every
+    kernel, each equal to the oracle."""
     if size == 9000 and n > 4096:
         n = 16384
     seed = 61
@@ -105,16 +103,18 @@ def test_small_batches_every_schedule(gpu, monkeypatch, n, size, rss):
 
 
 @pytest.mark.parametrize("key,nq,endian", [(None, 8, 1), ("ms", 16, 0), ("ms", 5, 1)])
-def test_wave_toeplitz_both_keys(gpu, monkeypatch, key, nq, endian):
-    """The wave kernel's lane-parallel Toeplitz (key windows from the key
-    words, no table) for both keys of util/rss.c."""
+@pytest.mark.parametrize("sched", ["wave", "row"])
+def test_small_kernels_toeplitz_both_keys(gpu, monkeypatch, key, nq, endian, sched):
+    """RSS in the small-batch kernels — the wave kernel's lane-parallel
+    Toeplitz (key windows from the key words, no table), the grouped kernels'
+    LDS tables — for both keys of util/rss.c."""
     k = oracle.KEY_MICROSOFT if key == "ms" else None
     n, seed = 8192, 62
     desc, nbytes = pktgen.layout(n, "bimodal", 6, seed)
     buf = np.zeros(nbytes, np.uint8)
     oracle.pktgen(buf, desc, 6, seed, 0)
     want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(k, nq, endian))
-    with ctx_for(gpu, monkeypatch, "wave", rss=True, rss_key=k, rss_queues=nq,
+    with ctx_for(gpu, monkeypatch, sched, rss=True, rss_key=k, rss_queues=nq,
                  rss_endian=bool(endian)) as ctx:
         got = run_rx_dev(ctx, buf, desc, 6)
     assert_same(got, want, f"toeplitz key={key} nq={nq} endian={endian}")
@@ -202,7 +202,8 @@ def test_fused_flow_bins_equal_separate_pass(gpu, size, n):
     assert (bins.cpu().numpy().view(np.uint32) != 0xFFFFFFFF).mean() > 0.99
 
 
-def test_tx_fill_ptrs_golden(gpu, golden):
+@pytest.mark.parametrize("sched", ["wave", "row", "quad"])
+def test_tx_fill_ptrs_golden(gpu, golden, monkeypatch, sched):
     """mtcp_gpu_tx_fill_ptrs (host frames, e.g. a DPDK m_table burst) and
     _dev (device-accessible frames): exactly the reference's fills, and only
     the two check fields of the filled frames change."""
@@ -210,7 +211,7 @@ def test_tx_fill_ptrs_golden(gpu, golden):
     offs = golden.desc["offset"].astype(np.int64)
     want = golden.buf.copy()
     assert oracle.tx_fill(want, golden.desc, 0) == golden.manifest["tx_filled"]
-    with gpu.Context(0) as ctx:
+    with ctx_for(gpu, monkeypatch, sched) as ctx:
         host = golden.buf.copy()
         assert ctx.tx_fill_ptrs(host, offs, golden.desc["len"]) == golden.manifest["tx_filled"]
         assert np.array_equal(host, want)

@@ -1,8 +1,8 @@
-"""Per-launch time of the two rx shapes over batch sizes: the wave kernel
-(one wavefront per packet, rx_wave.hpp) and rx_kernel's schedules (64
-packets per wave), each forced with MTCP_GPU_WAVE_UPTO at context open, on
+"""Per-launch time of every rx kernel over batch sizes — a wavefront, a row
+or a quad per packet (rx_wave.hpp), rx_kernel (64 packets per wave) — each
+forced with MTCP_GPU_SCHED at context open, and the dispatched choice, on
 the same frames; HIP events on the launch stream over back-to-back launches.
-The crossover sets mtcp_gpu.hip kWaveUpToPkts.
+The crossovers set mtcp_gpu.hip pick_sched.
   python tools/small_batch_probe.py [sizes...]    (default: 64 1500 bimodal 9000)
 """
 import json
@@ -20,7 +20,7 @@ dev = torch.device("cuda", 0)
 st = torch.cuda.Stream(dev)
 torch.cuda.set_stream(st)
 sizes = [s if s == "bimodal" else int(s) for s in sys.argv[1:]] or [64, 1500, "bimodal", 9000]
-NS = [64, 256, 1024, 4096, 16384, 32768, 65536, 131072, 262144]
+NS = [64, 1024, 4096, 16384, 32768, 65536, 131072]
 for size in sizes:
     for n in NS:
         desc, nbytes = pktgen.layout(n, size, 6, 7)
@@ -31,8 +31,8 @@ for size in sizes:
         frame_bytes = int(desc["len"].astype(np.int64).sum())
         line = {"size": size, "n": n, "frame_bytes": frame_bytes}
         ref = None
-        for sched, upto in (("wave", str(1 << 31)), ("rows", "0")):
-            os.environ["MTCP_GPU_WAVE_UPTO"] = upto
+        for sched in ("wave", "row", "quad", "big", "auto"):
+            os.environ["MTCP_GPU_SCHED"] = sched
             with gpu.Context(0, rss=size == "bimodal", rss_queues=8) as ctx:
                 for _ in range(10):
                     ctx.rx_chunk_dev(b, d, n, 6, o, stream=st)
@@ -50,7 +50,7 @@ for size in sizes:
                 rec = o.cpu()
                 if ref is None:
                     ref = rec
-                line["records_equal"] = bool(torch.equal(ref, rec))
-        os.environ.pop("MTCP_GPU_WAVE_UPTO", None)
+                line["records_equal"] = line.get("records_equal", True) and bool(torch.equal(ref, rec))
+        os.environ.pop("MTCP_GPU_SCHED", None)
         print(json.dumps(line), flush=True)
         del b, d, o
