@@ -18,12 +18,17 @@
  *     packets the reference's software checksums drop with ERROR
  *     (ip_in.c:35-36, tcp_in.c:1167-1173), the dpdk_get_rptr pattern for
  *     NIC-verified checksums (dpdk_module.c:473-479);
+ *   - MTCP_GPU_V_TRUNCATED -> NULL: a header claims bytes past the frame, so
+ *     the reference's checks would read past len (undefined) and no checksum
+ *     was computed that dev_ioctl's 0 could vouch for;
  *   - every other verdict -> the frame, and mTCP's own code takes its usual
  *     branch (the checks before and around the checksums stay in mTCP), with
  *     dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answering 0
  *     (ip_in.c:29-31, tcp_in.c:1160-1164) so the checksum is not recomputed.
  *
- * One rxq per mTCP thread, like its mtcp_gpu_ctx; not re-entrant.
+ * An rxq's copies and kernel run on its context's stream (mtcp_gpu_stream),
+ * with its own completion event; one context per mTCP thread, its rxqs used
+ * by that thread only (not re-entrant).
  */
 #ifndef MTCP_GPU_RXQ_H
 #define MTCP_GPU_RXQ_H
@@ -71,7 +76,7 @@ int  mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q);
 int  mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n);
 
 /* get_rptr for flushed frame i: the staged frame and its length, or NULL for
- * the checksum failures listed above.  *res (may be NULL) receives the
+ * the verdicts listed above.  *res (may be NULL) receives the
  * frame's full result record. */
 uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
                           const mtcp_gpu_result **res);

@@ -296,6 +296,11 @@ hipStream_t pick(mtcp_gpu_ctx *ctx, void *stream) {
 }
 
 int stage_reserve(Stage &s, uint64_t bytes, uint32_t pkts) {
+    // a stage's stream exists once a host call uses the stage (a context
+    // that only launches device-resident work, or serves an io_module's
+    // rxqs, has the one stream of mtcp_gpu_open)
+    if (!s.stream && !HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)))
+        return MTCP_GPU_EIO;
     // growing frees buffers that the stage's previous batch may still use:
     // drain that batch first rather than rely on hipFree's implicit sync
     if ((bytes > s.buf_cap || pkts > s.pkt_cap) && s.stream && !HIP_OK(hipStreamSynchronize(s.stream)))
@@ -387,9 +392,6 @@ int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rs
         !HIP_OK(hipMalloc(&ctx->d_count, sizeof(uint32_t))) ||
         !HIP_OK(hipMemcpy(ctx->d_rss_tables, tables, sizeof(tables), hipMemcpyHostToDevice)))
         rc = MTCP_GPU_ENOMEM;
-    for (int s = 0; s < kStages && rc == MTCP_GPU_OK; ++s)
-        if (!HIP_OK(hipStreamCreateWithFlags(&ctx->stage[s].stream, hipStreamNonBlocking)))
-            rc = MTCP_GPU_EIO;
     if (rc != MTCP_GPU_OK) {
         mtcp_gpu_close(ctx);
         return rc;

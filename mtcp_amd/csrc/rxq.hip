@@ -4,12 +4,14 @@
 // answered from the staging copy.  Host code only; the checksums run in the
 // rx kernel behind mtcp_gpu_rx_chunk_dev.
 //
-// Each rxq owns a device copy of its staging and a stream: a flush is one
-// H2D of [first frame, end of the descriptors) — the descriptors are copied
-// right behind the frames in the pinned buffer so that frames and
-// descriptors travel in one transfer — the kernel, and one D2H of the
-// results, so that flush_async / wait can overlap the GPU with the
-// backend's own work.
+// Each rxq owns a device copy of its staging and a completion event; its
+// work goes on its context's stream (one stream per mTCP thread, however
+// many interfaces and aggregates it stages): a flush is one H2D of [first
+// frame, end of the descriptors) — the descriptors are copied right behind
+// the frames in the pinned buffer so that frames and descriptors travel in
+// one transfer — the kernel, and one D2H of the results, then the event, so
+// that flush_async / wait can overlap the GPU with the backend's own work and
+// a wait does not wait for a later aggregate queued behind it.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -23,7 +25,8 @@
 struct mtcp_gpu_rxq {
     mtcp_gpu_ctx *ctx = nullptr;
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;        // the context's (not owned)
+    hipEvent_t evt = nullptr;            // recorded after a flush's D2H
     uint8_t *buf = nullptr;              // pinned staging: frames, then room for descriptors
     mtcp_gpu_desc *desc = nullptr;       // pinned
     mtcp_gpu_result *res = nullptr;      // pinned
@@ -32,7 +35,7 @@ struct mtcp_gpu_rxq {
     uint32_t max_pkts = 0;
     uint64_t max_bytes = 0;
     uint32_t n = 0;                      // frames staged
-    uint32_t done = 0;                   // frames with results
+    uint32_t done_n = 0;                 // frames with results
     uint32_t inflight = 0;               // frames of an unfinished flush_async (0: none)
     uint64_t used = 0;                   // staging bytes in use
 };
@@ -72,8 +75,9 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     q->device = dev;
     q->max_pkts = max_pkts;
     q->max_bytes = (max_bytes + 63) & ~63ull;
+    q->stream = reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx));
     const uint64_t staging = q->max_bytes + (uint64_t)max_pkts * sizeof(mtcp_gpu_desc);
-    if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
+    if (hipEventCreateWithFlags(&q->evt, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&q->buf, staging, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&q->desc, (size_t)max_pkts * sizeof(mtcp_gpu_desc), hipHostMallocDefault) !=
             hipSuccess ||
@@ -108,9 +112,9 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
 void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q) {
     if (!q) return;
     RxqDevice dg(q->device);
-    if (q->stream) {
-        (void)hipStreamSynchronize(q->stream);
-        (void)hipStreamDestroy(q->stream);
+    if (q->evt) {
+        if (q->inflight) (void)hipEventSynchronize(q->evt);
+        (void)hipEventDestroy(q->evt);
     }
     if (q->buf) (void)hipHostFree(q->buf);
     if (q->desc) (void)hipHostFree(q->desc);
@@ -125,7 +129,7 @@ int mtcp_gpu_rxq_push(mtcp_gpu_rxq *q, const uint8_t *frame, uint16_t len) {
     const uint64_t slot = ((uint64_t)len + 63) & ~63ull;
     if (q->inflight) return MTCP_GPU_EINVAL;       // staging is being read by the GPU
     if (q->n == q->max_pkts || q->used + slot > q->max_bytes) return MTCP_GPU_ENOSPC;
-    if (q->done) return MTCP_GPU_EINVAL;           // flushed frames not yet reset
+    if (q->done_n) return MTCP_GPU_EINVAL;           // flushed frames not yet reset
     mtcp_gpu_desc &d = q->desc[q->n];
     d.offset = (uint32_t)(q->used >> 6);           // 64 B units (off_shift 6)
     d.len = len;
@@ -147,14 +151,14 @@ int mtcp_gpu_rxq_push_chunk(mtcp_gpu_rxq *q, const uint8_t *buf, const mtcp_gpu_
     return MTCP_GPU_OK;
 }
 
-uint32_t mtcp_gpu_rxq_pending(const mtcp_gpu_rxq *q) { return q ? q->n - q->done : 0; }
+uint32_t mtcp_gpu_rxq_pending(const mtcp_gpu_rxq *q) { return q ? q->n - q->done_n : 0; }
 
 int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
     if (!q || q->inflight) return MTCP_GPU_EINVAL;
-    if (q->n == q->done) return MTCP_GPU_OK;
+    if (q->n == q->done_n) return MTCP_GPU_OK;
     RxqDevice dg(q->device);
     if (!dg.ok) return MTCP_GPU_ENODEV;
-    const uint32_t first = q->done, cnt = q->n - q->done;
+    const uint32_t first = q->done_n, cnt = q->n - q->done_n;
     // frames staged since the last flush: their descriptors are relative to
     // the staging base; the descriptors go right behind the frames
     const uint64_t lo = (uint64_t)q->desc[first].offset << 6;
@@ -168,8 +172,9 @@ int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
                                    reinterpret_cast<const mtcp_gpu_desc *>(q->d_buf + q->used), cnt,
                                    6, q->d_out, q->stream);
     if (rc == MTCP_GPU_OK &&
-        hipMemcpyAsync(q->res + first, q->d_out, (size_t)cnt * sizeof(mtcp_gpu_result),
-                       hipMemcpyDeviceToHost, q->stream) != hipSuccess)
+        (hipMemcpyAsync(q->res + first, q->d_out, (size_t)cnt * sizeof(mtcp_gpu_result),
+                        hipMemcpyDeviceToHost, q->stream) != hipSuccess ||
+         hipEventRecord(q->evt, q->stream) != hipSuccess))
         rc = MTCP_GPU_EIO;
     if (rc != MTCP_GPU_OK) {
         (void)hipStreamSynchronize(q->stream);
@@ -184,13 +189,13 @@ int mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n) {
     int rc = MTCP_GPU_OK;
     if (q->inflight) {
         RxqDevice dg(q->device);
-        if (hipStreamSynchronize(q->stream) == hipSuccess)
-            q->done += q->inflight;
+        if (hipEventSynchronize(q->evt) == hipSuccess)
+            q->done_n += q->inflight;
         else
             rc = MTCP_GPU_EIO;
         q->inflight = 0;
     }
-    if (n) *n = q->done;
+    if (n) *n = q->done_n;
     return rc;
 }
 
@@ -198,7 +203,7 @@ int mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n) {
     if (!q) return MTCP_GPU_EINVAL;
     const int rc = mtcp_gpu_rxq_flush_async(q);
     if (rc != MTCP_GPU_OK) {
-        if (n) *n = q->done;
+        if (n) *n = q->done_n;
         return rc;
     }
     return mtcp_gpu_rxq_wait(q, n);
@@ -206,12 +211,16 @@ int mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n) {
 
 uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
                           const mtcp_gpu_result **res) {
-    if (!q || i >= q->done) return nullptr;
+    if (!q || i >= q->done_n) return nullptr;
     const mtcp_gpu_result &r = q->res[i];
     if (len) *len = q->desc[i].len;
     if (res) *res = &r;
-    if (r.verdict == MTCP_GPU_V_IP_CSUM_BAD || r.verdict == MTCP_GPU_V_TCP_CSUM_BAD)
-        return nullptr;                            // core.c:774-775: rx_errors++
+    // core.c:774-775 counts NULL as rx_errors: the checksum failures, and the
+    // frames whose headers claim bytes past the frame (the reference would
+    // read past len there; the GPU computed no checksum to vouch for them)
+    if (r.verdict == MTCP_GPU_V_IP_CSUM_BAD || r.verdict == MTCP_GPU_V_TCP_CSUM_BAD ||
+        r.verdict == MTCP_GPU_V_TRUNCATED)
+        return nullptr;
     return q->buf + ((uint64_t)q->desc[i].offset << 6);
 }
 
@@ -223,7 +232,7 @@ uint8_t *mtcp_gpu_rxq_frame(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len) {
 
 void mtcp_gpu_rxq_reset(mtcp_gpu_rxq *q) {
     if (!q || q->inflight) return;                 // a flush_async is reading the staging
-    q->n = q->done = 0;
+    q->n = q->done_n = 0;
     q->used = 0;
 }
 

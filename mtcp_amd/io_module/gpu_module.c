@@ -1,19 +1,22 @@
 /*
  * gpu_module.c — the "gpu" I/O module for mTCP: an
  * io_module_func backend (mtcp/src/include/io_module.h:56-68) that wraps the
- * real driver backend (psio or dpdk), aggregates its receive bursts, checks
- * them on the MI355X in one launch and answers mTCP's checksum offload hook.
+ * real driver backend (psio or dpdk), checks received frames on the MI355X
+ * in aggregated launches, fills transmitted frames' checksums on it, and
+ * answers mTCP's checksum offload hooks.
  *
- * Built inside the mTCP tree, against its headers (mtcp.h, io_module.h) and
- * include/mtcp_gpu.h + include/mtcp_gpu_rxq.h; link -lmtcp_gpu.  Wiring, as
- * for the other backends (io_module.h:93-112, config.c:569-570):
+ * Built inside the mTCP tree, against its headers (mtcp.h, io_module.h,
+ * tcp_util.h) and include/mtcp_gpu.h + include/mtcp_gpu_rxq.h; link
+ * -lmtcp_gpu.  Wiring, as for the other backends (io_module.h:93-112,
+ * config.c:569-570):
  *
  *     extern io_module_func gpu_module_func;
  *     AssignIOModule: else if (!strcmp(m, "gpu")) current_iomodule_func = &gpu_module_func;
  *     mtcp.conf:      io = gpu   (+ the wrapped backend in gpu_inner_module)
  *
- * mTCP must be built WITHOUT --disable-hwcsum so that ProcessIPv4Packet and
- * ProcessTCPPacket ask dev_ioctl first (ip_in.c:28-31, tcp_in.c:1159-1164).
+ * mTCP must be built WITHOUT --disable-hwcsum so that it asks dev_ioctl
+ * first (ip_in.c:28-31, tcp_in.c:1159-1164, ip_out.c:147-161,
+ * tcp_out.c:320-324).
  *
  * Receive (RunMainLoop, core.c:763-777): recv_pkts pulls up to
  * GPU_AGG_BURSTS bursts from the wrapped backend, copying each frame into
@@ -21,33 +24,54 @@
  * receive: psio_module.c:244-246, dpdk_module.c:395-398), and runs the rx
  * kernel once over the aggregate.  Pipelined (the default): each interface
  * has two rxqs; recv_pkts starts the GPU on the aggregate it just gathered
- * and returns the PREVIOUS aggregate, checked meanwhile, so that the GPU's
- * copies and kernel overlap the gathering and mTCP's processing (one
- * aggregate of added latency; the first call of a burst returns 0, which
- * RunMainLoop's poll loop simply repeats; an aggregate is returned by the
- * next call even when nothing new arrives).  MTCP_GPU_PIPELINE=0 in the
- * environment: gather, check and return the same aggregate in one call.
- * get_rptr then serves the staged frames and returns NULL for the frames
- * whose IP or TCP
+ * and returns the PREVIOUS aggregate, checked meanwhile (one aggregate of
+ * added latency; the first call of a burst returns 0, which RunMainLoop's
+ * poll loop simply repeats; an aggregate is returned by the next call even
+ * when nothing new arrives).  MTCP_GPU_PIPELINE=0 in the environment:
+ * gather, check and return the same aggregate in one call.  get_rptr then
+ * serves the staged frames and returns NULL for the frames whose IP or TCP
  * checksum fails — the packets mTCP's software path drops with ERROR
- * (ip_in.c:35-36, tcp_in.c:1167-1173) — which core.c:774-775 counts as
- * rx_errors, the pattern dpdk_get_rptr uses for NIC-verified checksums
- * (dpdk_module.c:473-479).  dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM)
- * answers 0 while the GPU path is healthy and -1 after any GPU error, so
- * mTCP falls back to its own checksums exactly as with a NIC that lacks the
- * offload (dpdk_dev_ioctl, dpdk_module.c:809-816).
+ * (ip_in.c:35-36, tcp_in.c:1167-1173) — and for the frames whose headers
+ * claim more bytes than the frame holds (the reference would read past the
+ * frame there); core.c:774-775 counts them as rx_errors, the pattern
+ * dpdk_get_rptr uses for NIC-verified checksums (dpdk_module.c:473-479).
+ * dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers 0 while the GPU path
+ * of that interface is healthy and -1 otherwise, so mTCP falls back to its
+ * own checksums exactly as with a NIC that lacks the offload
+ * (dpdk_dev_ioctl, dpdk_module.c:809-816).
+ * NETSTAT difference: a frame dropped here never reaches ProcessPacket, so
+ * it counts in rx_errors only, while the --disable-hwcsum path also counts
+ * it in rx_packets / rx_bytes (eth_in.c:20-23) — as for dpdk_get_rptr's
+ * NIC-verified drops.
  *
- * Transmit is passed through and checksummed by mTCP (dev_ioctl answers -1
- * for the tx commands): the wrapped backend owns the tx chunk layout.  A
- * psio-specific build can call mtcp_gpu_tx_fill on ppc->w_chunk_buf before
- * psio_send_pkts and answer 0 for PKT_TX_IP_CSUM / PKT_TX_TCPIP_CSUM.
+ * Transmit, with MTCP_GPU_TX=1 in the environment: dev_ioctl
+ * (PKT_TX_TCPIP_CSUM_PEEK / PKT_TX_TCPIP_CSUM) answers 0, so mTCP leaves
+ * iph->check and tcph->check for the device; get_wptr records every frame
+ * it hands out, and send_pkts fills the recorded frames' checksums on the
+ * GPU (mtcp_gpu_tx_fill_ptrs: only the two check fields are written) before
+ * the wrapped backend sends them.  ICMP's IP checksum (PKT_TX_IP_CSUM) stays
+ * with mTCP.  If the GPU fails at send time, the recorded frames are filled
+ * with mTCP's own ip_fast_csum / TCPCalcChecksum and every later answer is
+ * -1.  Off by default: send_pkts is synchronous and mTCP calls it every loop
+ * with at most a burst (64 frames on DPDK, MAX_PKT_BURST), so each send pays
+ * a GPU round trip (gather, H2D, kernel, D2H) that costs more than the CPU's
+ * own fill of 64 frames (measured: DESIGN.md §7).
+ *
+ * Resources per mTCP thread: one GPU context (one HIP stream), and, for each
+ * of the CONFIG.eths_num interfaces (mtcp.h:138), two rxqs (pinned staging
+ * of GPU_AGG_BURSTS x GPU_BURST frames of up to GPU_FRAME_MAX bytes each,
+ * plus a device copy), created at init_handle, off the data path (a pinned
+ * allocation and a stream's first copies take milliseconds); an interface
+ * whose rxqs cannot be created runs on the wrapped backend alone.  Nothing
+ * here calls exit().
  */
 #include <stdlib.h>
 #include <string.h>
 
 #include "mtcp.h"
 #include "io_module.h"
-#include "debug.h"
+#include "debug.h"            /* brings tcp_in.h: struct iphdr / tcphdr, ntohs */
+#include "tcp_util.h"
 
 #include "mtcp_gpu.h"
 #include "mtcp_gpu_rxq.h"
@@ -56,35 +80,60 @@
 #define GPU_BURST      64                 /* PS_CHUNK_SIZE / MAX_PKT_BURST   */
 #define GPU_RXQ_PKTS   (GPU_AGG_BURSTS * GPU_BURST)
 #define GPU_FRAME_MAX  2048ull            /* MAX_PACKET_SIZE (ps.h:173)      */
+#define GPU_TX_MAX     4096               /* frames recorded between two send_pkts */
 
 /* the backend being wrapped (e.g. &ps_module_func or &dpdk_module_func) */
 io_module_func *gpu_inner_module;
+
+/* One receiving interface: two aggregates (pipelined; synchronous uses [0]). */
+struct gpu_ifq {
+    mtcp_gpu_rxq *rxq[2];
+    uint8_t dropped[2][GPU_RXQ_PKTS];     /* inner get_rptr gave NULL */
+    uint32_t count[2];                    /* frames gathered          */
+    int launched[2];                      /* on the GPU (flush_async went out) */
+    int served_raw[2];                    /* no verdicts: serve raw, ioctl -1 */
+    int pending;                          /* aggregate the next recv returns, -1 none */
+    int serving;                          /* aggregate get_rptr answers from */
+};
+
+/* Frames handed out by get_wptr since the last send_pkts of an interface. */
+struct gpu_txq {
+    uint8_t *pkt[GPU_TX_MAX];
+    uint16_t len[GPU_TX_MAX];
+    uint32_t n;
+};
 
 struct gpu_private_context {
     void *inner;                          /* the wrapped backend's context   */
     mtcp_gpu_ctx *gpu;                    /* NULL: software checksums        */
     int passthrough;                      /* no GPU at init: the inner backend */
     int pipeline;                         /* serve aggregate k while k+1 is checked */
-    /* per rx interface, two aggregates (pipelined; synchronous uses [0]) */
-    mtcp_gpu_rxq *rxq[MAX_DEVICES][2];
-    uint8_t dropped[MAX_DEVICES][2][GPU_RXQ_PKTS];   /* inner get_rptr gave NULL */
-    uint32_t count[MAX_DEVICES][2];       /* frames gathered                 */
-    int launched[MAX_DEVICES][2];         /* on the GPU (flush_async went out) */
-    int served_raw[MAX_DEVICES][2];       /* no verdicts: serve raw, ioctl -1 */
-    int pending[MAX_DEVICES];             /* aggregate the next recv returns, -1 none */
-    int serving[MAX_DEVICES];             /* aggregate get_rptr answers from */
+    int tx;                               /* tx checksums filled here        */
+    struct gpu_ifq *ifq[MAX_DEVICES];     /* created at init (or first recv_pkts) */
+    int ifq_failed[MAX_DEVICES];          /* no staging: this interface passes through */
+    struct gpu_txq *txq[MAX_DEVICES];
 };
+
+/* a context for threads whose own allocation failed: passthrough only */
+static __thread struct gpu_private_context gpu_fallback_ctx;
+
+static void gpu_ifq_wait(struct gpu_ifq *f)
+{
+    int b;
+    for (b = 0; b < 2; b++)
+        if (f->rxq[b])
+            (void)mtcp_gpu_rxq_wait(f->rxq[b], NULL);
+}
 
 /* After any GPU error: let the queued work finish, then software checksums
  * from now on (dev_ioctl answers -1). */
 static void gpu_fail(struct gpu_private_context *g)
 {
-    int i, b;
-    TRACE_ERROR("gpu_module: GPU rx failed; software checksums from now on\n");
+    int i;
+    TRACE_ERROR("gpu_module: GPU path failed; software checksums from now on\n");
     for (i = 0; i < MAX_DEVICES; i++)
-        for (b = 0; b < 2; b++)
-            if (g->rxq[i][b])
-                (void)mtcp_gpu_rxq_wait(g->rxq[i][b], NULL);
+        if (g->ifq[i])
+            gpu_ifq_wait(g->ifq[i]);
     if (g->gpu)
         mtcp_gpu_close(g->gpu);
     g->gpu = NULL;
@@ -114,36 +163,67 @@ static void gpu_load_module(void)
     gpu_inner_module->load_module();
 }
 
+/* The rx state of interface ifidx (created at init for CONFIG.eths_num
+ * interfaces, on first use for any other); NULL: the interface runs on the
+ * wrapped backend alone. */
+static struct gpu_ifq *gpu_ifq_get(struct gpu_private_context *g, int ifidx)
+{
+    struct gpu_ifq *f = g->ifq[ifidx];
+    int b;
+
+    if (f || g->ifq_failed[ifidx] || !g->gpu)
+        return f;
+    f = calloc(1, sizeof(*f));
+    for (b = 0; f && b < (g->pipeline ? 2 : 1); b++)
+        if (mtcp_gpu_rxq_create(&f->rxq[b], g->gpu, GPU_RXQ_PKTS,
+                                GPU_RXQ_PKTS * GPU_FRAME_MAX) != MTCP_GPU_OK) {
+            TRACE_ERROR("gpu_module: no staging for interface %d; it runs on the wrapped backend\n",
+                        ifidx);
+            mtcp_gpu_rxq_destroy(f->rxq[0]);
+            free(f);
+            f = NULL;
+        }
+    if (!f) {
+        g->ifq_failed[ifidx] = 1;
+        return NULL;
+    }
+    f->pending = f->serving = -1;
+    g->ifq[ifidx] = f;
+    return f;
+}
+
 static void gpu_init_handle(struct mtcp_thread_context *ctx)
 {
     struct gpu_private_context *g = calloc(1, sizeof(*g));
     const char *pl = getenv("MTCP_GPU_PIPELINE");
-    int i, b, ndev;
+    const char *tx = getenv("MTCP_GPU_TX");
+    int ndev, i;
 
-    if (!g) {
-        TRACE_ERROR("gpu_module: out of memory\n");
-        exit(EXIT_FAILURE);
-    }
     gpu_inner_module->init_handle(ctx);       /* sets ctx->io_private_context */
+    if (!g) {
+        TRACE_ERROR("gpu_module: out of memory; running on the wrapped backend\n");
+        g = &gpu_fallback_ctx;
+        memset(g, 0, sizeof(*g));
+        g->passthrough = 1;
+    }
     g->inner = ctx->io_private_context;
     ctx->io_private_context = g;
+    if (g->passthrough)
+        return;
     g->pipeline = !(pl && strcmp(pl, "0") == 0);
-    for (i = 0; i < MAX_DEVICES; i++)
-        g->pending[i] = g->serving[i] = -1;
+    g->tx = tx && strcmp(tx, "1") == 0;
 
     ndev = mtcp_gpu_device_count();
-    if (ndev <= 0 || mtcp_gpu_open(&g->gpu, ctx->cpu % ndev, NULL, 1, 0) != MTCP_GPU_OK) {
+    if (ndev <= 0 || mtcp_gpu_open(&g->gpu, ctx->cpu % ndev, NULL, 1, 0) != MTCP_GPU_OK ||
+        mtcp_gpu_reserve(g->gpu, 0, 0) != MTCP_GPU_OK) {     /* load the kernels now */
+        if (g->gpu)
+            mtcp_gpu_close(g->gpu);
         g->gpu = NULL;
         g->passthrough = 1;                  /* behave exactly like the inner */
         return;
     }
-    for (i = 0; i < MAX_DEVICES; i++)
-        for (b = 0; b < (g->pipeline ? 2 : 1); b++)
-            if (mtcp_gpu_rxq_create(&g->rxq[i][b], g->gpu, GPU_RXQ_PKTS,
-                                    GPU_RXQ_PKTS * GPU_FRAME_MAX) != MTCP_GPU_OK) {
-                TRACE_ERROR("gpu_module: no pinned staging\n");
-                exit(EXIT_FAILURE);
-            }
+    for (i = 0; i < CONFIG.eths_num && i < MAX_DEVICES; i++)
+        (void)gpu_ifq_get(g, i);
 }
 
 static int32_t gpu_link_devices(struct mtcp_thread_context *ctx)
@@ -154,28 +234,100 @@ static int32_t gpu_link_devices(struct mtcp_thread_context *ctx)
 static void gpu_release_pkt(struct mtcp_thread_context *ctx, int ifidx,
                             unsigned char *pkt_data, int len)
 {
-    struct gpu_private_context *g = ctx->io_private_context;
-    /* staged copies need no release; the originals went back at recv time */
-    if (g->passthrough)
+    /* always the wrapped backend's: psio hands the frame to the host stack
+     * (psio_release_pkt, psio_module.c:122-132, copies from pkt_data, here
+     * the staged copy); dpdk's is a no-op */
+    if (gpu_inner_module->release_pkt)
         INNER_VOID(ctx, gpu_inner_module->release_pkt(ctx, ifidx, pkt_data, len));
+}
+
+/* ---- transmit --------------------------------------------------------------- */
+
+/* mTCP's own fills (ip_out.c:164, tcp_out.c:327-329) for the frames the GPU
+ * did not fill; the same rule as mtcp_gpu_tx_fill (include/mtcp_gpu.h). */
+static void gpu_tx_fill_sw(uint8_t *pkt, uint16_t len)
+{
+    struct iphdr *iph = (struct iphdr *)(pkt + 14);
+    uint16_t proto = (uint16_t)((pkt[12] << 8) | pkt[13]);
+    unsigned int ihl, doff, tot_len;
+    struct tcphdr *tcph;
+
+    if (len < 34 || proto != 0x0800)
+        return;
+    ihl = iph->ihl;
+    tot_len = ntohs(iph->tot_len);
+    if (iph->version != 4 || ihl < 5 || iph->protocol != 6 || len < 14 + 4 * ihl + 20)
+        return;
+    tcph = (struct tcphdr *)(pkt + 14 + 4 * ihl);
+    doff = tcph->doff;
+    if (doff < 5 || tot_len < 4 * (ihl + doff) || 14 + tot_len > len)
+        return;
+    iph->check = 0;
+    iph->check = ip_fast_csum(iph, ihl);
+    tcph->check = 0;
+    tcph->check = TCPCalcChecksum((uint16_t *)tcph, (uint16_t)(tot_len - 4 * ihl),
+                                  iph->saddr, iph->daddr);
+}
+
+/* Fill the checksums of the frames recorded for interface nif. */
+static void gpu_tx_flush(struct gpu_private_context *g, int nif)
+{
+    struct gpu_txq *t = g->txq[nif];
+    uint32_t i;
+
+    if (!t || !t->n)
+        return;
+    if (g->gpu &&
+        mtcp_gpu_tx_fill_ptrs(g->gpu, t->pkt, t->len, t->n, NULL) != MTCP_GPU_OK)
+        gpu_fail(g);
+    if (!g->gpu)                              /* mTCP skipped these: fill them here */
+        for (i = 0; i < t->n; i++)
+            gpu_tx_fill_sw(t->pkt[i], t->len[i]);
+    t->n = 0;
 }
 
 static uint8_t *gpu_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uint16_t len)
 {
-    return INNER_CALL(ctx, gpu_inner_module->get_wptr(ctx, ifidx, len));
+    struct gpu_private_context *g = ctx->io_private_context;
+    uint8_t *p = INNER_CALL(ctx, gpu_inner_module->get_wptr(ctx, ifidx, len));
+    struct gpu_txq *t;
+
+    if (!p || g->passthrough || !g->tx)
+        return p;
+    t = g->txq[ifidx];
+    if (!t) {
+        t = g->txq[ifidx] = calloc(1, sizeof(*t));
+        if (!t) {
+            /* nowhere to record it, and mTCP has been told the device fills
+             * it: from now on mTCP computes tx checksums */
+            g->tx = 0;
+            return p;
+        }
+    }
+    if (t->n == GPU_TX_MAX)
+        gpu_tx_flush(g, ifidx);
+    t->pkt[t->n] = p;
+    t->len[t->n] = len;
+    t->n++;
+    return p;
 }
 
 static int32_t gpu_send_pkts(struct mtcp_thread_context *ctx, int nif)
 {
+    struct gpu_private_context *g = ctx->io_private_context;
+    if (!g->passthrough)
+        gpu_tx_flush(g, nif);
     return INNER_CALL(ctx, gpu_inner_module->send_pkts(ctx, nif));
 }
 
+/* ---- receive ---------------------------------------------------------------- */
+
 /* Pull up to GPU_AGG_BURSTS bursts from the wrapped backend into aggregate
  * a of interface ifidx and start the GPU on it; returns the frame count. */
-static uint32_t gather(struct mtcp_thread_context *ctx, int ifidx, int a)
+static uint32_t gather(struct mtcp_thread_context *ctx, struct gpu_ifq *f, int ifidx, int a)
 {
     struct gpu_private_context *g = ctx->io_private_context;
-    mtcp_gpu_rxq *q = g->rxq[ifidx][a];
+    mtcp_gpu_rxq *q = f->rxq[a];
     uint32_t total = 0;
     int b, i;
 
@@ -187,7 +339,7 @@ static uint32_t gather(struct mtcp_thread_context *ctx, int ifidx, int a)
         for (i = 0; i < n && total < GPU_RXQ_PKTS; i++) {
             uint16_t len = 0;
             uint8_t *p = INNER_CALL(ctx, gpu_inner_module->get_rptr(ctx, ifidx, i, &len));
-            g->dropped[ifidx][a][total] = (p == NULL);
+            f->dropped[a][total] = (p == NULL);
             if (mtcp_gpu_rxq_push(q, p, p ? len : 0) != MTCP_GPU_OK)
                 break;
             total++;
@@ -195,11 +347,11 @@ static uint32_t gather(struct mtcp_thread_context *ctx, int ifidx, int a)
         if (n < GPU_BURST || total + GPU_BURST > GPU_RXQ_PKTS)
             break;                                   /* nothing more waiting */
     }
-    g->count[ifidx][a] = total;
-    g->launched[ifidx][a] = 0;
+    f->count[a] = total;
+    f->launched[a] = 0;
     if (total && g->gpu) {
         if (mtcp_gpu_rxq_flush_async(q) == MTCP_GPU_OK)
-            g->launched[ifidx][a] = 1;
+            f->launched[a] = 1;
         else
             gpu_fail(g);
     }
@@ -207,15 +359,14 @@ static uint32_t gather(struct mtcp_thread_context *ctx, int ifidx, int a)
 }
 
 /* Wait for aggregate a's verdicts (served raw if it has none). */
-static void finish(struct gpu_private_context *g, int ifidx, int a)
+static void finish(struct gpu_private_context *g, struct gpu_ifq *f, int a)
 {
     uint32_t n_done = 0;
-    g->served_raw[ifidx][a] = 1;
-    if (!g->launched[ifidx][a])
+    f->served_raw[a] = 1;
+    if (!f->launched[a])
         return;
-    if (mtcp_gpu_rxq_wait(g->rxq[ifidx][a], &n_done) == MTCP_GPU_OK &&
-        n_done == g->count[ifidx][a] && g->gpu)
-        g->served_raw[ifidx][a] = 0;
+    if (mtcp_gpu_rxq_wait(f->rxq[a], &n_done) == MTCP_GPU_OK && n_done == f->count[a] && g->gpu)
+        f->served_raw[a] = 0;
     else
         gpu_fail(g);
 }
@@ -223,43 +374,45 @@ static void finish(struct gpu_private_context *g, int ifidx, int a)
 static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 {
     struct gpu_private_context *g = ctx->io_private_context;
+    struct gpu_ifq *f = g->passthrough ? NULL : gpu_ifq_get(g, ifidx);
     int a, p;
     uint32_t total;
 
-    if (g->passthrough)
+    if (!f)
         return INNER_CALL(ctx, gpu_inner_module->recv_pkts(ctx, ifidx));
     if (!g->pipeline) {
-        total = gather(ctx, ifidx, 0);
-        finish(g, ifidx, 0);
-        g->serving[ifidx] = 0;
+        total = gather(ctx, f, ifidx, 0);
+        finish(g, f, 0);
+        f->serving = 0;
         return (int32_t)total;
     }
     /* mTCP is done with the aggregate served last time: gather into the
      * one not on the GPU, start it, then return the one that is */
-    p = g->pending[ifidx];
+    p = f->pending;
     a = p >= 0 ? 1 - p : 0;
-    total = gather(ctx, ifidx, a);
-    g->pending[ifidx] = total ? a : -1;
-    g->serving[ifidx] = p;
+    total = gather(ctx, f, ifidx, a);
+    f->pending = total ? a : -1;
+    f->serving = p;
     if (p < 0)
         return 0;                                    /* filling the pipeline */
-    finish(g, ifidx, p);
-    return (int32_t)g->count[ifidx][p];
+    finish(g, f, p);
+    return (int32_t)f->count[p];
 }
 
 static uint8_t *gpu_get_rptr(struct mtcp_thread_context *ctx, int ifidx, int index,
                              uint16_t *len)
 {
     struct gpu_private_context *g = ctx->io_private_context;
+    struct gpu_ifq *f = g->passthrough ? NULL : g->ifq[ifidx];
     int a;
-    if (g->passthrough)
+    if (!f)
         return INNER_CALL(ctx, gpu_inner_module->get_rptr(ctx, ifidx, index, len));
-    a = g->serving[ifidx];
-    if (a < 0 || g->dropped[ifidx][a][index])
+    a = f->serving;
+    if (a < 0 || f->dropped[a][index])
         return NULL;
-    if (g->served_raw[ifidx][a])
-        return mtcp_gpu_rxq_frame(g->rxq[ifidx][a], (uint32_t)index, len);
-    return mtcp_gpu_rxq_get(g->rxq[ifidx][a], (uint32_t)index, len, NULL);
+    if (f->served_raw[a])
+        return mtcp_gpu_rxq_frame(f->rxq[a], (uint32_t)index, len);
+    return mtcp_gpu_rxq_get(f->rxq[a], (uint32_t)index, len, NULL);
 }
 
 static int32_t gpu_select(struct mtcp_thread_context *ctx)
@@ -273,32 +426,46 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
     int i;
 
     for (i = 0; i < MAX_DEVICES; i++) {
-        mtcp_gpu_rxq_destroy(g->rxq[i][0]);        /* NULL-safe; waits for its stream */
-        mtcp_gpu_rxq_destroy(g->rxq[i][1]);
+        gpu_tx_flush(g, i);                          /* frames still recorded */
+        free(g->txq[i]);
+        if (g->ifq[i]) {
+            mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[0]);   /* NULL-safe; waits for its work */
+            mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[1]);
+            free(g->ifq[i]);
+        }
     }
     if (g->gpu)
         mtcp_gpu_close(g->gpu);
     INNER_VOID(ctx, gpu_inner_module->destroy_handle(ctx));
     ctx->io_private_context = g->inner;
-    free(g);
+    if (g != &gpu_fallback_ctx)
+        free(g);
 }
 
 static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp)
 {
     struct gpu_private_context *g = ctx->io_private_context;
+    struct gpu_ifq *f;
 
-    switch (cmd) {
-    case PKT_RX_IP_CSUM:
-    case PKT_RX_TCP_CSUM:
-        /* verified on the GPU at recv time: bad frames never reach mTCP */
-        if (g->passthrough)
+    if (!g->passthrough && nif >= 0 && nif < MAX_DEVICES) {
+        switch (cmd) {
+        case PKT_RX_IP_CSUM:
+        case PKT_RX_TCP_CSUM:
+            /* verified on the GPU at recv time: bad frames never reach mTCP */
+            f = g->ifq[nif];
+            if (f)
+                return (g->gpu && f->serving >= 0 && !f->served_raw[f->serving]) ? 0 : -1;
+            break;                                   /* a passthrough interface */
+        case PKT_TX_TCPIP_CSUM_PEEK:
+        case PKT_TX_TCPIP_CSUM:
+            /* filled on the GPU at send_pkts (ICMP's PKT_TX_IP_CSUM stays with mTCP) */
+            return g->gpu && g->tx ? 0 : -1;
+        case PKT_TX_IP_CSUM:
+        case PKT_TX_TCP_CSUM:
+            return -1;
+        default:
             break;
-        return (g->gpu && g->serving[nif] >= 0 && !g->served_raw[nif][g->serving[nif]]) ? 0 : -1;
-    default:
-        if (!g->passthrough && (cmd == PKT_TX_IP_CSUM || cmd == PKT_TX_TCP_CSUM ||
-                                cmd == PKT_TX_TCPIP_CSUM || cmd == PKT_TX_TCPIP_CSUM_PEEK))
-            return -1;                        /* tx: mTCP computes (see above) */
-        break;
+        }
     }
     if (gpu_inner_module->dev_ioctl == NULL)
         return -1;

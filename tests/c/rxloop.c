@@ -9,12 +9,18 @@
  * those as rx_errors) and whether a served frame is byte-identical to the
  * original; dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers are logged.
  *
- *   rxloop CHUNK DESC OUT [timing|verify] [THREADS]
+ *   rxloop CHUNK DESC OUT [timing|verify|tx] [THREADS]
  *     CHUNK  frame bytes; DESC mtcp_gpu_desc records (byte offsets)
  *     OUT    one byte per frame: 0 NULL, 1 served intact, 2 served but changed
  *     timing served frames are not compared (only their first 64 B are read,
  *            as ProcessPacket's parse would): the loop's rate without the
  *            harness's own byte-for-byte check
+ *     tx     the transmit side instead: every frame of the chunk goes out
+ *            through get_wptr (copied in as mTCP's EthernetOutput would
+ *            write it), dev_ioctl(PKT_TX_TCPIP_CSUM_PEEK) decides who fills
+ *            the checksums (-1: the harness fills them, as mTCP's software
+ *            path, ip_out.c:164 / tcp_out.c:327-329), send_pkts every 64
+ *            frames (MAX_PKT_BURST); OUT = the sent frames, laid out as CHUNK
  *     THREADS  mTCP threads (default 1), one per core as core.c:1057 runs
  *            them: each has its own mtcp_thread_context (cpu = thread index),
  *            so its own gpu_module context, GPU ctx and staging, and its own
@@ -34,8 +40,19 @@
 #include "mtcp.h"
 #include "io_module.h"
 #include "mtcp_gpu.h"
+#include "tcp_util.h"
+#include "../../oracle/mtcp_oracle.h"
+
+/* mTCP's checksum functions, which gpu_module.c calls for frames the GPU
+ * could not fill (ps.h:66-95, tcp_util.c:157-190): the oracle's restatement */
+uint16_t ip_fast_csum(const void *iph, unsigned int ihl) { return oracle_ip_fast_csum(iph, ihl); }
+uint16_t TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t daddr)
+{
+    return oracle_tcp_calc_checksum(buf, len, saddr, daddr);
+}
 
 extern io_module_func gpu_module_func;
+struct mtcp_config CONFIG = {1};                   /* one interface (mtcp.conf's port list) */
 extern io_module_func *gpu_inner_module;
 
 struct fake_psio {
@@ -43,6 +60,9 @@ struct fake_psio {
     const mtcp_gpu_desc *desc;
     uint32_t n, next, base, cnt;
     int recv_calls;
+    uint8_t *tx_buf;                 /* tx: frame i is written at desc[i].offset */
+    uint32_t tx_next, tx_queued, tx_sent;
+    int send_calls;
 };
 static __thread struct fake_psio *tl_fake;         /* this thread's backend */
 
@@ -55,10 +75,24 @@ static void fake_release(struct mtcp_thread_context *ctx, int ifidx, unsigned ch
 }
 static uint8_t *fake_wptr(struct mtcp_thread_context *ctx, int ifidx, uint16_t len)
 {
-    (void)ctx; (void)ifidx; (void)len;
-    return NULL;
+    struct fake_psio *f = ctx->io_private_context;
+    (void)ifidx;
+    if (f != tl_fake) { fprintf(stderr, "context swap broken\n"); exit(3); }
+    if (!f->tx_buf || f->tx_next >= f->n || len != f->desc[f->tx_next].len)
+        return NULL;
+    f->tx_queued++;
+    return f->tx_buf + f->desc[f->tx_next++].offset;
 }
-static int32_t fake_send(struct mtcp_thread_context *ctx, int nif) { (void)ctx; (void)nif; return 0; }
+static int32_t fake_send(struct mtcp_thread_context *ctx, int nif)
+{
+    struct fake_psio *f = ctx->io_private_context;
+    (void)nif;
+    if (f != tl_fake) { fprintf(stderr, "context swap broken\n"); exit(3); }
+    f->send_calls++;
+    f->tx_sent += f->tx_queued;        /* the frames already sit in tx_buf */
+    f->tx_queued = 0;
+    return 0;
+}
 static int32_t fake_recv(struct mtcp_thread_context *ctx, int ifidx)
 {
     struct fake_psio *f = ctx->io_private_context;    /* must be the inner's */
@@ -106,17 +140,38 @@ static void *slurp(const char *path, size_t *size)
 
 struct worker {
     pthread_t tid;
-    int cpu, timing;
+    int cpu, timing, tx;
     struct fake_psio fake;                 /* frames [first, first + fake.n) */
     uint32_t first;
     uint8_t *status;                       /* status + first */
     uint64_t rx_packets, rx_errors, changed, hdr_sum;
-    int rounds, ioctl_ip, ioctl_tcp;
+    int rounds, ioctl_ip, ioctl_tcp, ioctl_tx, sw_filled;
     uint32_t seen;
     struct timespec t1;
 };
 static pthread_barrier_t g_start;
 static struct timespec g_t0;
+
+/* The transmit side of RunMainLoop: EthernetOutput's get_wptr, IPOutput /
+ * SendTCPPacket's dev_ioctl and software fills, then send_pkts per burst. */
+static void tx_main(struct worker *w, struct mtcp_thread_context *ctx)
+{
+    const struct fake_psio *f = &w->fake;
+    uint32_t i;
+    for (i = 0; i < f->n; i++) {
+        const mtcp_gpu_desc *d = &f->desc[i];
+        uint8_t *p = gpu_module_func.get_wptr(ctx, 0, d->len);
+        if (!p) { fprintf(stderr, "get_wptr refused frame %u\n", i); exit(4); }
+        memcpy(p, f->buf + d->offset, d->len);
+        w->ioctl_tx = gpu_module_func.dev_ioctl(ctx, 0, PKT_TX_TCPIP_CSUM_PEEK, p + 14);
+        if (w->ioctl_tx == -1) {                         /* mTCP fills them itself */
+            mtcp_gpu_desc one = {0, d->len, 0, 0};
+            w->sw_filled += (int)oracle_tx_fill(p, d->len, &one, 1, 0);
+        }
+        if ((i + 1) % 64 == 0 || i + 1 == f->n)
+            gpu_module_func.send_pkts(ctx, 0);
+    }
+}
 
 static void *worker_main(void *arg)
 {
@@ -131,6 +186,12 @@ static void *worker_main(void *arg)
     if (pthread_barrier_wait(&g_start) == PTHREAD_BARRIER_SERIAL_THREAD)
         clock_gettime(CLOCK_MONOTONIC, &g_t0);
     pthread_barrier_wait(&g_start);                  /* g_t0 set before anyone runs */
+    if (w->tx) {
+        tx_main(w, &ctx);
+        clock_gettime(CLOCK_MONOTONIC, &w->t1);
+        gpu_module_func.destroy_handle(&ctx);
+        return NULL;
+    }
     for (int idle = 0;;) {                            /* core.c:763-777 */
         int32_t recv_cnt = gpu_module_func.recv_pkts(&ctx, 0), i;
         if (recv_cnt <= 0) {
@@ -196,12 +257,15 @@ int main(int argc, char **argv)
         return 1;
     }
     timing = argc > 4 && strcmp(argv[4], "timing") == 0;
+    int tx = argc > 4 && strcmp(argv[4], "tx") == 0;
+    uint8_t *tx_buf = NULL;
     threads = argc > 5 ? atoi(argv[5]) : 1;
     if (threads < 1 || threads > 64) { fprintf(stderr, "THREADS: 1..64\n"); return 1; }
     buf = slurp(argv[1], &nb);
     desc = slurp(argv[2], &nd);
     n = (uint32_t)(nd / sizeof(mtcp_gpu_desc));
     status = calloc(n + 1, 1);
+    if (tx) tx_buf = calloc(nb + 64, 1);
     ws = calloc((size_t)threads, sizeof(*ws));
 
     gpu_inner_module = &fake_module;
@@ -213,6 +277,8 @@ int main(int argc, char **argv)
         const uint32_t hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
         w->cpu = t;
         w->timing = timing;
+        w->tx = tx;
+        w->fake.tx_buf = tx_buf;
         w->first = lo;
         w->status = status + lo;
         w->fake.buf = buf;
@@ -238,6 +304,22 @@ int main(int argc, char **argv)
     for (uint32_t k = 0; k < n; k++) frame_bytes += desc[k].len;
 
     out = fopen(argv[3], "wb");
+    if (tx) {
+        int sw = 0, sends = 0;
+        uint32_t sent = 0;
+        for (t = 0; t < threads; t++) {
+            sw += ws[t].sw_filled;
+            sends += ws[t].fake.send_calls;
+            sent += ws[t].fake.tx_sent;
+        }
+        if (!out || fwrite(tx_buf, 1, nb, out) != nb) { perror(argv[3]); return 1; }
+        fclose(out);
+        secs = (double)(t1.tv_sec - g_t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - g_t0.tv_nsec);
+        printf("{\"frames\": %u, \"sent\": %u, \"send_calls\": %d, \"ioctl_tx\": %d, "
+               "\"sw_filled\": %d, \"seconds\": %.6f, \"frame_bytes\": %llu, \"threads\": %d}\n",
+               n, sent, sends, ws[0].ioctl_tx, sw, secs, (unsigned long long)frame_bytes, threads);
+        return 0;
+    }
     if (!out || fwrite(status, 1, n, out) != n) { perror(argv[3]); return 1; }
     fclose(out);
     secs = (double)(t1.tv_sec - g_t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - g_t0.tv_nsec);

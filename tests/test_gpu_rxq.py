@@ -1,8 +1,9 @@
 """include/mtcp_gpu_rxq.h on the GPU: frames pushed one by one (as
 gpu_module.c does with the wrapped backend's get_rptr pointers), checked by
 a synchronous flush or by flush_async + wait, served by rxq_get: NULL
-exactly for the checksum failures (ip_in.c:35-36, tcp_in.c:1167-1173), the
-staged frame byte for byte otherwise, and every result record equal to the
+exactly for the checksum failures (ip_in.c:35-36, tcp_in.c:1167-1173) and
+the frames whose headers claim bytes past the frame (TRUNCATED), the staged
+frame byte for byte otherwise, and every result record equal to the
 oracle's for the same frame."""
 import ctypes
 
@@ -14,7 +15,7 @@ from mtcp_amd import RESULT_DTYPE
 
 torch = pytest.importorskip("torch")
 
-V_IP_CSUM_BAD, V_TCP_CSUM_BAD, V_BAD_DESC = 4, 9, 11
+V_IP_CSUM_BAD, V_TCP_CSUM_BAD, V_TRUNCATED, V_BAD_DESC = 4, 9, 10, 11
 EINVAL = -22
 
 
@@ -60,7 +61,7 @@ def test_rxq_serves_the_oracle_verdicts(golden, mode):
                     got = np.frombuffer(ctypes.string_at(res.value, 40), dtype=RESULT_DTYPE)[0]
                     if want["verdict"][k] != V_BAD_DESC:
                         assert got.tobytes() == want[k].tobytes(), k
-                    drop = got["verdict"] in (V_IP_CSUM_BAD, V_TCP_CSUM_BAD)
+                    drop = got["verdict"] in (V_IP_CSUM_BAD, V_TCP_CSUM_BAD, V_TRUNCATED)
                     assert (p is None) == drop, k
                     assert ln.value == d["len"]
                     if p is not None:

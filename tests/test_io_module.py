@@ -6,8 +6,14 @@ CPU: the module compiles against mTCP's own headers (when /root/reference is
 present) and, without a GPU, passes every frame through untouched with
 dev_ioctl answering -1 (mTCP's software checksums, ip_in.c:29-31).
 GPU: get_rptr returns NULL exactly for the frames the reference drops on a
-checksum (ip_in.c:35-36, tcp_in.c:1167-1173), every other frame is served
-byte-identical, and dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers 0.
+checksum (ip_in.c:35-36, tcp_in.c:1167-1173) and for the frames whose
+headers claim bytes past the frame (TRUNCATED: the reference's "ref-UB"
+frames), every other frame is served byte-identical, and
+dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers 0.
+Transmit (the harness plays mTCP's EthernetOutput / IPOutput / SendTCPPacket,
+ip_out.c:147-165, tcp_out.c:320-330): the frames sent equal the reference's
+tx fills of the golden chunk, whoever fills them — the GPU at send_pkts
+(dev_ioctl(PKT_TX_TCPIP_CSUM_PEEK) 0) or mTCP's software path (-1).
 """
 import json
 import os
@@ -19,7 +25,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
 GOLD = os.path.join(ROOT, "tests", "golden")
-V_IP_CSUM_BAD, V_TCP_CSUM_BAD = 4, 9
+V_IP_CSUM_BAD, V_TCP_CSUM_BAD, V_TRUNCATED = 4, 9, 10
 
 
 def build_rxloop() -> str:
@@ -27,14 +33,32 @@ def build_rxloop() -> str:
     return os.path.join(ROOT, "tests", "c", "rxloop")
 
 
-def run_rxloop(tmp_path, threads=1, pipeline="1"):
+def run_rxloop(tmp_path, threads=1, pipeline="1", mode="verify", tx="0"):
     exe = build_rxloop()
     status = tmp_path / "status.bin"
     p = subprocess.run([exe, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
-                        str(status), "verify", str(threads)], capture_output=True, text=True,
-                       timeout=300, env=dict(os.environ, MTCP_GPU_PIPELINE=pipeline))
+                        str(status), mode, str(threads)], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX=tx))
     assert p.returncode == 0, p.stderr
     return json.loads(p.stdout.strip().splitlines()[-1]), np.fromfile(status, dtype=np.uint8)
+
+
+def tx_expect(golden):
+    """The golden chunk after the reference's tx fills, frame bytes only (the
+    harness writes each frame's len bytes into a zeroed buffer)."""
+    import oracle
+    full = np.fromfile(os.path.join(GOLD, "rx_buf.bin"), dtype=np.uint8)
+    assert oracle.tx_fill(full, golden.desc, 0) == golden.manifest["tx_filled"]
+    want = np.zeros_like(full)
+    for o, n in zip(golden.desc["offset"].astype(np.int64), golden.desc["len"].astype(np.int64)):
+        want[o:o + n] = full[o:o + n]
+    return want
+
+
+def rx_drops(golden):
+    import oracle
+    v = oracle.rx_chunk(golden.buf, golden.desc, 0)["verdict"]
+    return (v == V_IP_CSUM_BAD) | (v == V_TCP_CSUM_BAD) | (v == V_TRUNCATED)
 
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "mtcp", "src", "include")),
@@ -65,18 +89,28 @@ def test_passthrough_without_gpu(tmp_path):
     assert stats["ioctl_rx_ip"] == -1 and stats["ioctl_rx_tcp"] == -1
 
 
+def test_tx_passthrough_without_gpu(tmp_path, golden):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    stats, sent = run_rxloop(tmp_path, mode="tx")
+    assert stats["ioctl_tx"] == -1 and stats["sw_filled"] == golden.manifest["tx_filled"]
+    assert stats["sent"] == stats["frames"] == len(golden.desc)
+    assert np.array_equal(sent, tx_expect(golden))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("pipeline", ["1", "0"])
 def test_gpu_module_drops_exactly_the_checksum_failures(tmp_path, golden, pipeline):
-    import oracle
     stats, status = run_rxloop(tmp_path, pipeline=pipeline)
-    v = oracle.rx_chunk(golden.buf, golden.desc, 0)["verdict"]
-    drop = (v == V_IP_CSUM_BAD) | (v == V_TCP_CSUM_BAD)
+    drop = rx_drops(golden)
     assert stats["seen"] == stats["frames"] == len(golden.desc)
     assert np.array_equal(status == 0, drop)
     assert (status[~drop] == 1).all() and stats["changed"] == 0
     assert stats["rx_errors"] == int(drop.sum()) > 100
-    # on the reference's own verdicts (not ref-UB): the same set
+    # on the reference's own verdicts (not ref-UB, which are the TRUNCATED
+    # frames dropped above): the same set
+    assert np.array_equal(drop & (golden.meta["ref_ub"] == 1), golden.meta["ref_ub"] == 1)
     ok = golden.meta["ref_ub"] == 0
     ref_drop = (golden.expect["verdict"] == V_IP_CSUM_BAD) | (golden.expect["verdict"] == V_TCP_CSUM_BAD)
     assert np.array_equal(drop[ok], ref_drop[ok])
@@ -91,13 +125,32 @@ def test_gpu_module_one_context_per_thread(tmp_path, golden, pipeline):
     """mTCP's share-nothing threads (core.c:1057): four threads, each with its
     own mtcp_thread_context, gpu_module context, GPU ctx and staging, over
     contiguous shards of the chunk, drop exactly the single-thread set."""
-    import oracle
     stats, status = run_rxloop(tmp_path, threads=4, pipeline=pipeline)
-    v = oracle.rx_chunk(golden.buf, golden.desc, 0)["verdict"]
-    drop = (v == V_IP_CSUM_BAD) | (v == V_TCP_CSUM_BAD)
+    drop = rx_drops(golden)
     assert stats["threads"] == 4
     assert stats["seen"] == stats["frames"] == len(golden.desc)
     assert np.array_equal(status == 0, drop)
     assert (status[~drop] == 1).all() and stats["changed"] == 0
     assert stats["rx_errors"] == int(drop.sum())
     assert stats["ioctl_rx_ip"] == 0 and stats["ioctl_rx_tcp"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 4])
+def test_gpu_module_fills_tx_checksums(tmp_path, golden, threads):
+    """MTCP_GPU_TX=1: dev_ioctl(PKT_TX_TCPIP_CSUM_PEEK) answers 0, mTCP leaves
+    the checks to the device, and the frames send_pkts hands the wrapped backend carry
+    exactly the reference's fills (GPU, at 64-frame bursts)."""
+    stats, sent = run_rxloop(tmp_path, threads=threads, mode="tx", tx="1")
+    assert stats["ioctl_tx"] == 0 and stats["sw_filled"] == 0
+    assert stats["sent"] == stats["frames"] == len(golden.desc)
+    assert stats["send_calls"] >= len(golden.desc) // 64
+    assert np.array_equal(sent, tx_expect(golden))
+
+
+@pytest.mark.gpu
+def test_gpu_module_tx_off_leaves_checksums_to_mtcp(tmp_path, golden):
+    """The default (tx offload off): dev_ioctl answers -1 and mTCP fills."""
+    stats, sent = run_rxloop(tmp_path, mode="tx")
+    assert stats["ioctl_tx"] == -1 and stats["sw_filled"] == golden.manifest["tx_filled"]
+    assert np.array_equal(sent, tx_expect(golden))

@@ -6,9 +6,13 @@ into the rxq's pinned staging, 64 bursts (4096 frames) go to the GPU per
 launch (H2D, rx kernel, D2H of the records), and get_rptr serves the staged
 frames.  Frames come from the GPU generator (include/mtcp_gpu_pktgen.h),
 copied to host memory first.  Prints one JSON line per frame size and mode,
-then the timing mode with 2, 4 and 8 mTCP threads (one mtcp_thread_context,
-gpu_module context and GPU ctx each, contiguous shards: core.c:1057's
-share-nothing threads sharing one GPU).
+then the timing mode with 2, 4, 8 and 16 mTCP threads (one
+mtcp_thread_context, gpu_module context and GPU ctx each, contiguous shards:
+core.c:1057's share-nothing threads sharing one GPU), next to the
+reference's own rx code (oracle/_ref, compiled from /root/reference) on the
+same frames in the same run, 1 and 16 pinned cores; and the transmit side
+(rxloop tx: get_wptr / dev_ioctl / send_pkts per 64 frames) with the GPU
+filling the checksums and with mTCP filling them (MTCP_GPU_TX=0).
   usage: python tools/io_path_bench.py [n_frames]
          python tools/io_path_bench.py n_frames --dump DIR SIZE   (write the
              chunk and descriptor files rxloop reads for one frame size, e.g.
@@ -28,13 +32,37 @@ sys.path.insert(0, ROOT)
 from mtcp_amd import gpu, pktgen  # noqa: E402
 
 
-def run(n, size, seed, tmp, mode, threads=1, pipeline=True):
-    desc, nbytes = pktgen.layout(n, size, 6, seed)
-    dev = torch.device("cuda", 0)
-    d_buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
-    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
-    gpu.pktgen_dev(d_buf, d_desc, n, 6, seed)
-    host = d_buf.cpu().numpy()
+_frames = {}
+
+
+def frames(n, size, seed):
+    if (n, size, seed) not in _frames:
+        desc, nbytes = pktgen.layout(n, size, 6, seed)
+        dev = torch.device("cuda", 0)
+        d_buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+        gpu.pktgen_dev(d_buf, d_desc, n, 6, seed)
+        _frames[(n, size, seed)] = (desc, d_buf.cpu().numpy())
+    return _frames[(n, size, seed)]
+
+
+def reference(n, size, seed):
+    """The reference's own rx code (eth_in/ip_in/tcp_in/tcp_util compiled from
+    /root/reference into oracle/_ref) on the same frames: 1 and 16 cores."""
+    import oracle   # the CPU baseline leg only
+    if not oracle.ref_available():
+        return None
+    desc, host = frames(n, size, seed)
+    out = {"probe": "reference_rx", "frame_size": size, "frames": n}
+    nbytes = int(desc["len"].astype(np.int64).sum())
+    for cores in (1, 16):
+        t = oracle.ref_bench_rx(host.copy(), desc, 6, False, cores, 5)
+        out[f"cores{cores}"] = {"mpkt_per_s": round(n / t / 1e6, 3), "GBs": round(nbytes / t / 1e9, 3)}
+    return out
+
+
+def run(n, size, seed, tmp, mode, threads=1, pipeline=True, tx=True):
+    desc, host = frames(n, size, seed)
     bdesc = desc.copy()
     bdesc["offset"] = desc["offset"] << 6          # rxloop takes byte offsets
     chunk, dpath, opath = (os.path.join(tmp, x) for x in ("chunk.bin", "desc.bin", "out.bin"))
@@ -43,13 +71,23 @@ def run(n, size, seed, tmp, mode, threads=1, pipeline=True):
     exe = os.path.join(ROOT, "tests", "c", "rxloop")
     best = None
     for _ in range(3):
-        env = dict(os.environ, MTCP_GPU_PIPELINE="1" if pipeline else "0")
+        env = dict(os.environ, MTCP_GPU_PIPELINE="1" if pipeline else "0", MTCP_GPU_TX="1" if tx else "0")
         r = subprocess.run([exe, chunk, dpath, opath, mode, str(threads)],
                            capture_output=True, text=True, check=True, env=env)
         st = json.loads(r.stdout.strip().splitlines()[-1])
         if best is None or st["seconds"] < best["seconds"]:
             best = st
     s = best["seconds"]
+    if mode == "tx":
+        return {"probe": "io_module_tx", "threads": threads, "gpu_fills": tx, "frame_size": size,
+                "frames": n, "seconds": s, "mpkt_per_s": round(n / s / 1e6, 3),
+                "GBs": round(best["frame_bytes"] / s / 1e9, 3), "ioctl_tx": best["ioctl_tx"],
+                "sw_filled": best["sw_filled"], "send_calls": best["send_calls"],
+                "note": "get_wptr + copy of the frame + dev_ioctl(PKT_TX_TCPIP_CSUM_PEEK) per frame, "
+                        "send_pkts per 64 frames; gpu_fills: mtcp_gpu_tx_fill_ptrs at send_pkts "
+                        "(gather, H2D, kernel, D2H of 8 B per frame, check fields written back), "
+                        "else mTCP's software fill per frame (here the oracle's restatement, "
+                        "gcc -O2); wall clock, best of 3"}
     return {"probe": "io_module_path", "mode": mode, "threads": threads, "pipeline": pipeline,
             "frame_size": size,
             "frames": n,
@@ -89,8 +127,16 @@ def main():
             for mode, pipeline in (("timing", True), ("timing", False), ("verify", True)):
                 print(json.dumps(run(n, size, seed, tmp, mode, 1, pipeline)), flush=True)
         for size, seed in ((1500, 2), (64, 1)):
-            for threads in (2, 4, 8):
+            for threads in (2, 4, 8, 16):
                 print(json.dumps(run(n, size, seed, tmp, "timing", threads)), flush=True)
+            ref = reference(n, size, seed)
+            if ref:
+                print(json.dumps(ref), flush=True)
+        for size, seed in ((1500, 2), (64, 1)):
+            for threads in (1, 4):
+                for tx in (True, False):
+                    print(json.dumps(run(min(n, 1 << 18), size, seed, tmp, "tx", threads, tx=tx)),
+                          flush=True)
 
 
 if __name__ == "__main__":
