@@ -139,6 +139,16 @@ uint32_t grid_for(const mtcp_gpu_ctx *ctx, uint32_t n) {
 constexpr uint64_t kUnrollBelowSlotBytes = 1024;
 constexpr uint64_t kLineAlignAboveSlotBytes = 1536;
 
+// Two workgroups share each CU, and the first one dispatched wins the memory
+// arbitration: per-wave s_memrealtime stamps of C2 (tools/rx_variants
+// stampsab) show the second workgroup ending ~7 us after the first, with
+// the CU half-occupied meanwhile.  The second workgroup runs at s_setprio(1)
+// for its first four passes (rx_kernel PRIO 5), which evens the two (C2:
+// 242.9-245.8 -> 239.7-240.8 us in the same process); the other schedules
+// showed no change and keep the default.
+template <int SCHED, bool LALIGN>
+constexpr int prio_for() { return SCHED == mg::kSchedUnrolled && !LALIGN ? 5 : 0; }
+
 template <int MODE, bool RSS, int SCHED, bool LALIGN>
 void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
     // tx fill streams its frames through L2 normally (NT off): its check-field
@@ -149,8 +159,9 @@ void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
     // backwards so neighbouring frames' shared lines are read in one step
     // (C5: 4.768 -> 4.737 GB per launch = chunk + descriptors, no line twice)
     constexpr bool kRev = LALIGN && SCHED == mg::kSchedUnrolled;
-    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, SCHED, LALIGN, 0, 8, 8, kNT, 6, kRev>), grid, block, 0,
-                       st, kp);
+    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, SCHED, LALIGN, 0, 8, 8, kNT, 6, kRev, false,
+                                      prio_for<SCHED, LALIGN>()>),
+                       grid, block, 0, st, kp);
 }
 
 // Small batches (one io_module aggregate is 4096 frames) give each wave one

@@ -82,6 +82,7 @@ struct KParams {
     uint32_t *fill_count;          // tx fill: frames written (may be null)
     uint32_t *bins;                // rx: HashFlow bin per packet (may be null)
     uint2 *tx_report;              // tx (wave kernel): {checks, T} per frame instead of writing them
+    uint32_t *stamps;              // profiling builds only (rx_kernel STAMP): 4 dwords per wave
     uint32_t rss_key[4];           // key bytes 0..15, big-endian words (wave kernel's Toeplitz)
 };
 
@@ -504,9 +505,22 @@ struct Trip {
 // rounds, round pairs, software-pipelined trips, per-pass stores interleaved
 // with the next pass's loads — lost on every config and were removed).
 // LALIGN: multi-trip frames stream from the start of their first 128 B line.
+// STAMP (profiling builds, tools/rx_variants.hip): lane 0 of each wave writes
+// {start, end} of s_memrealtime (100 MHz), HW_REG_XCC_ID and HW_REG_HW_ID to
+// kp.stamps[4 * wave ...].
+// PRIO: the second workgroup on each CU (blockIdx >= gridDim / 2; the
+// dispatcher fills every CU once before the second round) runs at
+// s_setprio(PRIO & 3): the older wave of a SIMD otherwise wins its issue
+// arbitration and finishes first; PRIO & 4: only for the first half of its
+// passes.
 template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
-          bool NT = true, int U = 6, bool REV = false>
+          bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
+    uint64_t t_start = 0;
+    if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
+    if constexpr ((PRIO & 3) > 0) {
+        if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(PRIO & 3);
+    }
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ WaveLds lds[kWavesPerBlock];
     if constexpr (RSS) {
@@ -834,6 +848,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     v4u va, vb;
     bool have_pre_small = false; // SCHED 6: already issued into va, vb
     for (uint32_t g0 = 0; g0 < kp.n; g0 += pass_pkts) {
+        if constexpr ((PRIO & 4) != 0) {
+            if (g0 == 4 * pass_pkts) __builtin_amdgcn_s_setprio(0);
+        }
         const Frame f = decode(g0);
         if (!__ballot(f.live)) break;
         fetch(g0 + pass_pkts);                                     // next pass's descriptors
@@ -1085,6 +1102,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
     flush();
     tx_flush();
+    if constexpr (STAMP) {
+        __builtin_amdgcn_s_waitcnt(0);                 // the wave's stores have left
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            uint32_t *st = kp.stamps + 4 * wave;
+            st[0] = (uint32_t)t_start;
+            st[1] = (uint32_t)t_end;
+            st[2] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);   // HW_REG_XCC_ID[3:0]
+            st[3] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+        }
+    }
 }
 
 }  // namespace mg

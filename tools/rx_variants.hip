@@ -413,12 +413,119 @@ int main(int argc, char **argv) {
         kp.lens = dl;
     }
 
+    if (argc > 3 && !strcmp(argv[3], "stampsab")) {
+        // The end-time classes (old / young workgroup on a CU, XCC) of several
+        // phase-1 layouts of the C2 kernel, and their launch times, one process.
+        using namespace mg;
+        struct SV { const char *name; kfn fn; };
+        const SV svs[] = {
+            {"B8", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, true>},
+            {"B16", rx_kernel<kRxChunk, false, 3, false, 0, 8, 16, true, 6, false, true>},
+            {"B32", rx_kernel<kRxChunk, false, 3, false, 0, 8, 32, true, 6, false, true>},
+            {"B64", rx_kernel<kRxChunk, false, 3, false, 0, 8, 64, true, 6, false, true>},
+            {"B8_prio1half", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, true, 5>},
+            {"B16_prio1half", rx_kernel<kRxChunk, false, 3, false, 0, 8, 16, true, 6, false, true, 5>},
+        };
+        const uint32_t groups = (n + 63) / 64;
+        const uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, cus * 2), waves = blocks * 4;
+        uint32_t *d_st;
+        CK(hipMalloc(&d_st, waves * 16));
+        kp.stamps = d_st;
+        kp.out = d_out;
+        std::vector<uint32_t> st(waves * 4);
+        std::vector<mtcp_gpu_result> ref(n), got(n);
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        for (int r = 0; r < rounds; ++r) {
+            for (size_t v = 0; v < sizeof(svs) / sizeof(svs[0]); ++v) {
+                for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(svs[v].fn, dim3(blocks), dim3(256), 0, 0, kp);
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(svs[v].fn, dim3(blocks), dim3(256), 0, 0, kp);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                CK(hipMemcpy(st.data(), d_st, waves * 16, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(got.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
+                if (v == 0) ref = got;
+                else if (memcmp(ref.data(), got.data(), n * sizeof(mtcp_gpu_result))) {
+                    fprintf(stderr, "%s records differ from B8's\n", svs[v].name);
+                    return 2;
+                }
+                uint32_t t0 = 0xFFFFFFFFu;
+                for (uint32_t w = 0; w < waves; ++w) t0 = std::min(t0, st[4 * w]);
+                double cls[2][8] = {{0}}; int cn[2][8] = {{0}}; double mx = 0, sum = 0;
+                for (uint32_t w = 0; w < waves; ++w) {
+                    const double e = (st[4 * w + 1] - t0) * 0.01;
+                    const int y = (w / 4) >= blocks / 2, x = st[4 * w + 2] & 7;
+                    cls[y][x] += e; cn[y][x]++; mx = std::max(mx, e); sum += e;
+                }
+                printf("{\"round\": %d, \"variant\": \"%s\", \"launch_us\": %.2f, \"end_mean\": %.2f, \"end_max\": %.2f, \"old_by_xcc\": [",
+                       r, svs[v].name, ms * 1e3 / 20, sum / waves, mx);
+                for (int x = 0; x < 8; ++x) printf("%s%.1f", x ? ", " : "", cn[0][x] ? cls[0][x] / cn[0][x] : 0.0);
+                printf("], \"young_by_xcc\": [");
+                for (int x = 0; x < 8; ++x) printf("%s%.1f", x ? ", " : "", cn[1][x] ? cls[1][x] / cn[1][x] : 0.0);
+                printf("]}\n");
+            }
+        }
+        return 0;
+    }
+    if (argc > 3 && !strcmp(argv[3], "stamps")) {
+        // Per-wave start/end of the dispatched kernel (rx_kernel STAMP): is the
+        // end-time spread systematic (by XCD, SE, CU, wave slot) or random?
+        using namespace mg;
+        const int prio = argc > 4 ? atoi(argv[4]) : 0;
+        kfn fn = rss ? (prio ? (kfn)rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, true, 1>
+                             : (kfn)rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, true>)
+                     : !strcmp(cfg, "c5") ? (kfn)rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, true>
+                     : prio ? (kfn)rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, true, 1>
+                            : (kfn)rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, true>;
+        const uint32_t groups = (n + 63) / 64;
+        uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, cus * 2);
+        const uint32_t waves = blocks * 4;
+        uint32_t *d_st;
+        CK(hipMalloc(&d_st, waves * 16));
+        kp.stamps = d_st;
+        kp.out = d_out;
+        std::vector<uint32_t> st(waves * 4);
+        for (int r = 0; r < rounds; ++r) {
+            for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, 0, kp);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(st.data(), d_st, waves * 16, hipMemcpyDeviceToHost));
+            uint32_t t0 = 0xFFFFFFFFu;
+            for (uint32_t w = 0; w < waves; ++w) t0 = std::min(t0, st[4 * w]);
+            // one line per wave of the last round only; a summary per round
+            std::vector<double> ends(waves);
+            double xe[16] = {0}; int xn[16] = {0};
+            for (uint32_t w = 0; w < waves; ++w) {
+                ends[w] = (st[4 * w + 1] - t0) * 0.01;    // us (100 MHz)
+                const uint32_t x = st[4 * w + 2] & 15;
+                xe[x] += ends[w]; xn[x]++;
+                if (r == rounds - 1)
+                    printf("{\"wave\": %u, \"start_us\": %.2f, \"end_us\": %.2f, \"xcc\": %u, \"hw_id\": %u}\n",
+                           w, (st[4 * w] - t0) * 0.01, ends[w], x, st[4 * w + 3]);
+            }
+            std::vector<double> e = ends;
+            std::sort(e.begin(), e.end());
+            printf("{\"round\": %d, \"end_p0\": %.2f, \"end_p10\": %.2f, \"end_p50\": %.2f, \"end_p90\": %.2f, \"end_p100\": %.2f, \"xcc_mean_end\": [",
+                   r, e[0], e[waves / 10], e[waves / 2], e[waves * 9 / 10], e[waves - 1]);
+            for (int x = 0; x < 8; ++x) printf("%s%.2f", x ? ", " : "", xn[x] ? xe[x] / xn[x] : 0.0);
+            printf("]}\n");
+        }
+        return 0;
+    }
     std::vector<Variant> vs;
     using namespace mg;
     if (rss) {
         // variant 0 = what mtcp_gpu.hip dispatches for C3; every other variant's
         // records must equal its records byte for byte
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
+        vs.push_back({"rss_sorted6_prio1half_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 5>, 2});
+        vs.push_back({"rss_sorted6_prio2half_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 6>, 2});
+        vs.push_back({"rss_sorted6_prio1_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 1>, 2});
+        vs.push_back({"rss_sorted6_prio2_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 2>, 2});
+        vs.push_back({"rss_sorted6_prio3_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 3>, 2});
         vs.push_back({"rss_sorted6_fullgrid", rx_kernel<kRxChunk, true, 6>, 1u << 20});
         vs.push_back({"rss_sorted6_cu4", rx_kernel<kRxChunk, true, 6>, 4});
         vs.push_back({"rss_sorted6_cu8", rx_kernel<kRxChunk, true, 6>, 8});
@@ -441,6 +548,13 @@ int main(int argc, char **argv) {
     } else {
         // variant 0 = what mtcp_gpu.hip dispatches for C2 (C5 adds LALIGN)
         vs.push_back({"unrolled_cu2", rx_kernel<kRxChunk, false, 3>, 2});
+        vs.push_back({"unrolled_prio1half_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 5>, 2});
+        vs.push_back({"unrolled_prio2half_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 6>, 2});
+        vs.push_back({"unrolled_lalign_rev_prio1half_cu2", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, false, 5>, 2});
+        vs.push_back({"unrolled_prio1_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 1>, 2});
+        vs.push_back({"unrolled_prio2_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 2>, 2});
+        vs.push_back({"unrolled_prio3_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 3>, 2});
+        vs.push_back({"unrolled_lalign_rev_prio1_cu2", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, false, 1>, 2});
         vs.push_back({"unrolled_fullgrid", rx_kernel<kRxChunk, false, 3>, 1u << 20});
         vs.push_back({"unrolled_cu4", rx_kernel<kRxChunk, false, 3>, 4});
         vs.push_back({"unrolled_cu8", rx_kernel<kRxChunk, false, 3>, 8});
