@@ -542,6 +542,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     const uint32_t lane_off = map(lane);
     const uint64_t safe = (uint64_t)(uintptr_t)(MODE == kRxPtrs ? (const void *)kp.out
                                                                : (const void *)kp.buf);
+    // the packet of this lane in pass g0, and whether the batch has it
+    auto lane_pkt = [&](uint32_t g0, bool &live) -> uint32_t {
+        live = g0 + lane_off < kp.n;
+        return g0 + lane_off;
+    };
 
     // ---------------- phase 0: descriptors (of the NEXT pass, prefetched) ---
     // The raw descriptor fields are loaded one pass ahead so that their
@@ -549,8 +554,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     uint64_t raw_a = 0;     // chunk mode: the 8-byte descriptor; ptrs mode: the pointer
     uint32_t raw_b = 0;     // ptrs mode: the length
     auto fetch = [&](uint32_t g0) {
-        const uint32_t k = g0 + lane_off;
-        if (k < kp.n) {
+        bool live;
+        const uint32_t k = lane_pkt(g0, live);
+        if (live) {
             if constexpr (MODE == kRxPtrs) {
                 raw_a = (uint64_t)(uintptr_t)kp.ptrs[k];
                 raw_b = kp.lens[k];
@@ -561,8 +567,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     };
     auto decode = [&](uint32_t g0) -> Frame {
         Frame f;
-        const uint32_t k = g0 + lane_off;
-        f.live = k < kp.n;
+        bool live;
+        (void)lane_pkt(g0, live);
+        f.live = live;
         f.p = safe;
         f.L = 0;
         f.ok = false;
@@ -780,8 +787,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                     // from the record itself (no register held for it), stored
                     // in runs of B consecutive packets
                     if (kp.bins) {
-                        const uint32_t rec = gq + map(lane);
-                        if (rec < kp.n)
+                        bool live;
+                        const uint32_t rec = lane_pkt(gq, live);
+                        if (live)
                             kp.bins[rec] = flow_bin(keep[q][0], keep[q][1], keep[q][2], keep[q][9] & 0xFFu);
                     }
                 }

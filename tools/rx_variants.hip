@@ -420,11 +420,7 @@ int main(int argc, char **argv) {
         struct SV { const char *name; kfn fn; };
         const SV svs[] = {
             {"B8", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, true>},
-            {"B16", rx_kernel<kRxChunk, false, 3, false, 0, 8, 16, true, 6, false, true>},
-            {"B32", rx_kernel<kRxChunk, false, 3, false, 0, 8, 32, true, 6, false, true>},
-            {"B64", rx_kernel<kRxChunk, false, 3, false, 0, 8, 64, true, 6, false, true>},
             {"B8_prio1half", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, true, 5>},
-            {"B16_prio1half", rx_kernel<kRxChunk, false, 3, false, 0, 8, 16, true, 6, false, true, 5>},
         };
         const uint32_t groups = (n + 63) / 64;
         const uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, cus * 2), waves = blocks * 4;
