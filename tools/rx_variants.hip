@@ -418,10 +418,21 @@ int main(int argc, char **argv) {
         // phase-1 layouts of the C2 kernel, and their launch times, one process.
         using namespace mg;
         struct SV { const char *name; kfn fn; };
-        const SV svs[] = {
+        const SV svs_c2[] = {
             {"B8", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, true>},
             {"B8_prio1half", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, true, 5>},
         };
+        const SV svs_c3[] = {
+            {"sorted6", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, true>},
+            {"sorted6_prio1half", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, true, 5>},
+            {"sorted6_prio2half", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, true, 6>},
+        };
+        const SV svs_c5[] = {
+            {"lalign_rev", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, true>},
+            {"lalign_rev_prio1half", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, true, 5>},
+        };
+        const SV *svs = rss ? svs_c3 : !strcmp(cfg, "c5") ? svs_c5 : svs_c2;
+        const size_t nsv = rss ? 3 : 2;
         const uint32_t groups = (n + 63) / 64;
         const uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, cus * 2), waves = blocks * 4;
         uint32_t *d_st;
@@ -434,7 +445,7 @@ int main(int argc, char **argv) {
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         for (int r = 0; r < rounds; ++r) {
-            for (size_t v = 0; v < sizeof(svs) / sizeof(svs[0]); ++v) {
+            for (size_t v = 0; v < nsv; ++v) {
                 for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(svs[v].fn, dim3(blocks), dim3(256), 0, 0, kp);
                 CK(hipEventRecord(e0));
                 for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(svs[v].fn, dim3(blocks), dim3(256), 0, 0, kp);
@@ -446,7 +457,7 @@ int main(int argc, char **argv) {
                 CK(hipMemcpy(got.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 if (v == 0) ref = got;
                 else if (memcmp(ref.data(), got.data(), n * sizeof(mtcp_gpu_result))) {
-                    fprintf(stderr, "%s records differ from B8's\n", svs[v].name);
+                    fprintf(stderr, "%s records differ from %s's\n", svs[v].name, svs[0].name);
                     return 2;
                 }
                 uint32_t t0 = 0xFFFFFFFFu;
