@@ -24,7 +24,7 @@ def fuzz_batch(n, seed, aligned):
             offs[i] = pos
             pos += (int(L[i]) + 63) & ~63
         else:
-            offs[i] = ((pos + 127) & ~127) + 4 * int(rng.integers(0, 32))
+            offs[i] = ((pos + 127) & ~127) + 2 * int(rng.integers(0, 64))   # any even start
             pos = offs[i] + int(L[i])
     buf = rng.integers(0, 256, ((pos + 127) & ~127) + 128, dtype=np.uint8)
 
