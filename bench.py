@@ -291,6 +291,18 @@ def run_row(args):
                             "algorithmic_bytes_per_launch": algo,
                             "note": "40 B record read (its 12 key bytes and verdict span the "
                                     "record's lines) + 4 B bin written per packet"}
+        # HashFlow fused into the rx pass (mtcp_gpu_rx_chunk_flow_dev): the
+        # bin leaves with the record, so the record is never read back
+        rx_step = lambda: ctx.rx_chunk_dev(d_buf, d_desc, n, 6, d_out, stream=stream)
+        fused_step = lambda: ctx.rx_chunk_flow_dev(d_buf, d_desc, n, 6, d_out, bins, stream=stream)
+        _, k_rx = _timed(rx_step, args.steps, args.warmup, stream)
+        _, k_fused = _timed(fused_step, args.steps, args.warmup, stream)
+        line["fused_rx_flow"] = {"rx_us": round(k_rx * 1e6, 2), "rx_flow_fused_us": round(k_fused * 1e6, 2),
+                                 "rx_then_flow_us": round((k_rx + kern) * 1e6, 2),
+                                 "saved_us": round((k_rx + kern - k_fused) * 1e6, 2),
+                                 "note": "HIP events per launch, C2 batch (1 M x 1500 B): rx alone, "
+                                         "rx with the bin fused, rx followed by the separate "
+                                         "flow_hash kernel"}
         if want_cpu:
             import oracle
             res = d_out.cpu().numpy().view(gpu.RESULT_DTYPE)
