@@ -239,11 +239,21 @@ int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_on
     return s;
 }
 
+// The wave kernel's loads per lane per trip: two (2 KiB, an MTU frame in one
+// trip) when the batch's average slot is at most 2 KiB, ten (10 KiB, a 9000 B
+// frame in one trip) otherwise; a longer frame takes more trips either way.
+// Pointer bursts count as 1 KiB slots: a DPDK mbuf's default data room is
+// 2 KiB (RTE_MBUF_DEFAULT_DATAROOM), so their frames fit the short trip.
+constexpr uint64_t kWaveShortUpToSlot = 2048;
+
 template <int MODE, bool RSS>
-void launch_small(int sched, uint32_t n, hipStream_t st, const mg::KParams &kp) {
+void launch_small(int sched, uint32_t n, uint64_t slot, hipStream_t st, const mg::KParams &kp) {
     if (sched == kSchedWave) {
-        hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS>), dim3((n + mg::kWavesPerBlock - 1) / mg::kWavesPerBlock),
-                           dim3(mg::kBlock), 0, st, kp);
+        const dim3 grid((n + mg::kWavesPerBlock - 1) / mg::kWavesPerBlock);
+        if (slot <= kWaveShortUpToSlot)
+            hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS, 0, 1, 2>), grid, dim3(mg::kBlock), 0, st, kp);
+        else
+            hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS>), grid, dim3(mg::kBlock), 0, st, kp);
     } else if (sched == kSchedQuad) {
         constexpr uint32_t P = mg::GroupShape<4>::P;
         hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 4>), dim3((n + P - 1) / P), dim3(mg::kGroupBlock), 0,
@@ -260,13 +270,13 @@ int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     if (kp.n == 0) return MTCP_GPU_OK;
     const bool rss = !mg::is_tx(MODE) && (ctx->flags & MTCP_GPU_F_RSS);
     const bool ptrs = MODE == mg::kRxPtrs || MODE == mg::kTxPtrs;
-    const int sched = pick_sched(ctx, kp.n, ptrs ? 1024 : kp.buf_len / kp.n,
-                                 MODE == mg::kTxPtrs || kp.tx_report != nullptr);
+    const uint64_t avg_slot = ptrs ? 1024 : kp.buf_len / kp.n;
+    const int sched = pick_sched(ctx, kp.n, avg_slot, MODE == mg::kTxPtrs || kp.tx_report != nullptr);
     if (sched != kSchedBig) {
         if (rss)
-            launch_small<MODE, true>(sched, kp.n, st, kp);
+            launch_small<MODE, true>(sched, kp.n, avg_slot, st, kp);
         else
-            launch_small<MODE, false>(sched, kp.n, st, kp);
+            launch_small<MODE, false>(sched, kp.n, avg_slot, st, kp);
         return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
     }
     if constexpr (MODE != mg::kTxPtrs) {

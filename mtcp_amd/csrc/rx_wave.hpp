@@ -60,8 +60,18 @@ __device__ __forceinline__ uint32_t toeplitz_wave(const uint32_t (&kw)[4], uint3
 }
 
 // ABL (profiling only, tools/wave_probe.hip): 1 = the frame stream and its
-// plain chunk sum only (lane 0 stores it); 2 = descriptor only (stores L).
-template <int MODE, bool RSS, int ABL = 0>
+// plain chunk sum only (lane 0 stores it); 2 = descriptor only (stores L);
+// 3 = stop after the header parse (stores the verdict); 4 = after the
+// segment sum (stores the TCP checksum).
+// SEG, the segment sum [T, 14 + ip_len): 1 = the plain sum of every chunk
+// minus the bytes outside the segment (the header bytes from LDS, the tail of
+// the last chunk from LDS), one lane per dword and one reduction, when the
+// segment runs to the frame's last chunk and the frame fits one trip; any
+// other frame, and SEG 0 always, masks each chunk against the segment.
+// NL: 16 B loads per lane per trip (a trip covers 1 KiB * NL of frame):
+// 2 for MTU-sized batches, kWaveLoads for jumbo ones (mtcp_gpu.hip picks by
+// the batch's average slot); fewer unrolled loads, fewer instructions.
+template <int MODE, bool RSS, int ABL = 0, int SEG = 1, int NL = kWaveLoads>
 __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
     __shared__ uint4 lds[kWavesPerBlock][kSlotChunks];     // the frame's chunks 0..6
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -95,11 +105,11 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
     }
 
     // ---- phase 1: the wave issues the frame's first trip (10 KiB) --------------------
-    constexpr uint32_t kTrip = kWave * kWaveLoads;
-    v4u x[kWaveLoads];
+    constexpr uint32_t kTrip = kWave * NL;
+    v4u x[NL];
     auto issue = [&](uint32_t c0) {
 #pragma unroll
-        for (int u = 0; u < kWaveLoads; ++u) {
+        for (int u = 0; u < NL; ++u) {
             if (c0 + u * kWave < nch) {                    // wave-uniform
                 const uint32_t c = c0 + u * kWave + lane;
                 x[u] = gload_nt(p16 + 16ull * (c < nch ? c : nch - 1));
@@ -112,7 +122,7 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
         for (uint32_t c0 = 0; c0 < nch; c0 += kTrip) {
             if (c0) issue(c0);
 #pragma unroll
-            for (int u = 0; u < kWaveLoads; ++u)
+            for (int u = 0; u < NL; ++u)
                 if (c0 + u * kWave < nch && c0 + u * kWave + lane < nch) acc = halves4(x[u], acc);
         }
         acc = row_sum(acc);
@@ -129,6 +139,24 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
     //      for 2-byte-aligned starts); the fields are readlanes of it, the IP
     //      header sum a 32-lane reduction, the verdict chain scalar code. ----------
     if (nch && lane < kSlotChunks - 1) hd4[lane] = make_uint4(x[0].x, x[0].y, x[0].z, x[0].w);
+    // SEG 1: the plain sum of every chunk of a one-trip frame, taken now so
+    // that the loads' registers are free during the parse, and the load that
+    // holds the last chunk (lane (nch - 1) % 64 of load (nch - 1) / 64)
+    uint32_t total = 0;
+    v4u last = {0u, 0u, 0u, 0u};
+    if constexpr (SEG == 1) {
+        if (nch <= kTrip) {
+            const uint32_t ul = (nch - 1) / kWave;
+#pragma unroll
+            for (int u = 0; u < NL; ++u) {
+                const uint32_t c = u * kWave + lane;
+                if ((uint32_t)u * kWave < nch) {
+                    if (c < nch) total = halves4(x[u], total);
+                    if (ul == (uint32_t)u) last = x[u];
+                }
+            }
+        }
+    }
     __builtin_amdgcn_wave_barrier();
     const uint32_t sh = (uint32_t)(p & 15);
     const uint32_t a = sh >> 2, fb = 8 * (sh & 3);
@@ -145,9 +173,41 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
         return (uint32_t)__builtin_amdgcn_readlane((int)r, 15) + (uint32_t)__builtin_amdgcn_readlane((int)r, 31);
     };
     Pkt pk = parse_head<MODE>(pd, ipsum, L, ok);
+    if constexpr (ABL == 3) {
+        if (lane == 0) kp.out[k].saddr = pk.verdict;
+        return;
+    }
 
     // ---- phase 2b: the segment [T, 14 + ip_len), summed by the lanes holding it --------
-    if (pk.need_sum) {
+    // SEG 1: the segment runs to the last chunk ([E, end of the chunk grid)
+    // lies inside it) and the frame is one trip
+    const uint32_t e_rel = sh + 14 + pk.ip_len;                      // byte E on the grid
+    const bool seg_fast = SEG == 1 && nch <= kTrip && ((e_rel + 15) >> 4) == nch;
+    if (pk.need_sum && seg_fast) {
+        uint32_t acc = total;
+        // bytes to remove, without branches: [0, sh + T) from the header
+        // dwords (lanes 0..22; the low half of dword `whole` when sh + T ends
+        // mid-dword) and [E, 16 * nch) from the last chunk, by its lane
+        const uint32_t nb = sh + pk.T, whole = nb >> 2, te = e_rel & 15;
+        const uint32_t v = hd[lane < 23 ? lane : 0u];
+        uint32_t w = lane < whole ? halves(v, 0u) : (lane == whole && (nb & 2)) ? (v & 0xFFFFu) : 0u;
+        const uint32_t d[4] = {last.x, last.y, last.z, last.w};
+        uint32_t t = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int drop = (int)te - 4 * j;                            // low bytes inside the segment
+            const uint32_t m = drop <= 0 ? 0xFFFFFFFFu : drop >= 4 ? 0u : (0xFFFFFFFFu << (8 * drop));
+            t = halves(d[j] & m, t);
+        }
+        w += (te && lane == (nch - 1) % kWave) ? t : 0u;
+        acc -= w;
+        acc = row_sum(acc);
+        const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)acc, 15) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 31) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 47) +
+                             (uint32_t)__builtin_amdgcn_readlane((int)acc, 63);
+        finish_seg<MODE>(pk, seg);
+    } else if (pk.need_sum) {
         const uint32_t lo = sh + pk.T, span = 14 + pk.ip_len - pk.T;   // bytes [lo, lo + span) of the grid
         uint32_t acc = 0;
         auto take = [&](const v4u &v, uint32_t c) {
@@ -168,9 +228,9 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
             }
         };
         for (uint32_t c0 = 0; c0 < nch; c0 += kTrip) {
-            if (c0) issue(c0);                              // jumbo frames: later trips
+            if (c0 || SEG == 1) issue(c0);                  // jumbo frames: later trips (SEG 1: all)
 #pragma unroll
-            for (int u = 0; u < kWaveLoads; ++u) {
+            for (int u = 0; u < NL; ++u) {
                 const uint32_t c = c0 + u * kWave + lane;
                 if (c0 + u * kWave < nch && c < nch) take(x[u], c);
             }
@@ -183,6 +243,10 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
         finish_seg<MODE>(pk, seg);
     }
 
+    if constexpr (ABL == 4) {
+        if (lane == 0) kp.out[k].saddr = pk.tcp_csum;
+        return;
+    }
     if constexpr (is_tx(MODE)) {
         if (lane == 0) {
             const uint32_t checks = fold_csum(pk.s_ip - pk.ip_check) | (pk.tcp_csum << 16);
@@ -234,10 +298,10 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
 // costs 1/P of the wave-uniform version's issue slots.
 constexpr int kGroupBlock = 1024;              // 16 waves
 
-template <int G>
+template <int G, int BLOCK = kGroupBlock>
 struct GroupShape {
     static_assert(G == 4 || G == 16 || G == 64, "lanes per packet: a quad, a row or the wave");
-    static constexpr int P = kGroupBlock / G;                   // packets per workgroup
+    static constexpr int P = BLOCK / G;                         // packets per workgroup
     static constexpr int U = G == 64 ? 8 : G == 16 ? 6 : 2;     // loads per lane per trip
     static constexpr int R = G >= 16 ? G / 16 : 1;              // partial sums per packet
     static constexpr int S = P + 1;                             // LDS stride (odd: no conflicts)
@@ -245,16 +309,20 @@ struct GroupShape {
 };
 
 // ABL (profiling only, tools/wave_probe.hip): 1 = phase 2 stores the sum only.
-template <int MODE, bool RSS, int G, int ABL = 0>
-__global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
-    using Sh = GroupShape<G>;
+// LOCAL: each wave parses its own kWave / G packets (no workgroup barrier),
+// for BLOCK = 256: a small batch then spreads over every CU (4 096 packets
+// with G = 16: one wave per SIMD) and phase 2 runs on every SIMD at once.
+template <int MODE, bool RSS, int G, int ABL = 0, int BLOCK = kGroupBlock, bool LOCAL = false>
+__global__ __launch_bounds__(BLOCK) void rx_group_kernel(KParams kp) {
+    using Sh = GroupShape<G, BLOCK>;
     constexpr int P = Sh::P, U = Sh::U, R = Sh::R, S = Sh::S;
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ uint32_t hd[kHdRows * S];       // dword i of packet q at hd[i * S + q]
     __shared__ uint32_t psum[P * R];
     __shared__ uint4 info[P];                  // {p lo, p hi, L | ok << 16, nch}
     if constexpr (RSS) {
-        for (int i = threadIdx.x; i < kRssTableWords; i += kGroupBlock) rss_lds[i] = kp.rss_tables[i];
+        for (int i = threadIdx.x; i < kRssTableWords; i += BLOCK) rss_lds[i] = kp.rss_tables[i];
+        if constexpr (LOCAL) __syncthreads();
     }
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wib = threadIdx.x >> 6;
@@ -324,11 +392,16 @@ __global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
         if ((lane & (kRow - 1)) == kRow - 1) psum[pkt * R + gl / kRow] = acc;
     }
     if (gl == 0) info[pkt] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), L | ((uint32_t)ok << 16), nch);
-    __syncthreads();
+    if constexpr (LOCAL) {
+        __builtin_amdgcn_wave_barrier();       // the wave's own packets: its LDS writes are in order
+    } else {
+        __syncthreads();
+    }
 
     // ---- phase 2: one lane per packet --------------------------------------------
-    if (wib >= (uint32_t)Sh::W2) return;
-    const uint32_t q = wib * kWave + lane;
+    if (!LOCAL && wib >= (uint32_t)Sh::W2) return;
+    if (LOCAL && lane >= (uint32_t)(kWave / G)) return;
+    const uint32_t q = LOCAL ? wib * (kWave / G) + lane : wib * kWave + lane;
     const uint32_t kk = blockIdx.x * P + q;
     if (q >= (uint32_t)P || kk >= kp.n) return;
     const uint4 inf = info[q];
