@@ -16,9 +16,14 @@
 //            reduction and four readlanes give the frame's chunk sum in an
 //            SGPR.  Chunks 0..6 (the headers) and the last chunk go to the
 //            wave's 128 B of LDS.
-//   phase 2  parse_finish (rx_kernels.hpp, the same code rx_kernel runs per
-//            lane) on the whole wave with wave-uniform operands: one
-//            instruction stream per packet, LDS reads broadcast.  RSS is the
+//   phase 2  parse_head / finish_seg (rx_kernels.hpp, the code rx_kernel
+//            runs per lane) on the whole wave with wave-uniform operands: one
+//            instruction stream per packet, mostly scalar.  The CU's one
+//            scalar unit serves its 16 waves of a 4 096-packet batch, so the
+//            SALU count per packet sets phase 2's time (PMC, 4 096 x 1500 B:
+//            ~190 SALU of phase 2 per wave ~ 1.3 us); the segment sum is
+//            therefore the plain chunk total (taken as the loads land) minus
+//            the header and tail bytes, branch-free in the lanes.  RSS is the
 //            Toeplitz sum spread over the lanes — lane i owns input bits i and
 //            64 + i, the key window of each bit comes straight from the key
 //            words (BuildKeyCache, util/rss.c:13-105, without the table), an
@@ -288,9 +293,9 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
 // a 4-lane quad for smaller frames), phase 2 with ONE LANE per packet.
 //
 // rx_wave_kernel above runs phase 2 on the whole wave with wave-uniform
-// operands, i.e. ~400 wave-instructions per packet: measured
-// (tools/wave_probe.hip) its phase 1 over 4 096 x 1500 B costs 2.6 us — the
-// launch floor, 2.5 us — and its phase 2 another 2.6 us, all VALU issue.  Here a
+// operands, i.e. ~400 wave-instructions per packet, scalar-unit bound when
+// many waves share a CU (tools/wave_probe.hip: phase 1 over 4 096 x 1500 B is
+// at the 2.3-2.6 us launch floor, the whole kernel 3.8 us).  Here a
 // 16-wave workgroup streams P = 1024 / G packets, leaves each packet's chunk
 // sum, header chunks, last chunk and descriptor in LDS (packet-minor, as in
 // rx_kernel), meets at one barrier, and then P lanes parse P packets in one
@@ -298,10 +303,10 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
 // costs 1/P of the wave-uniform version's issue slots.
 constexpr int kGroupBlock = 1024;              // 16 waves
 
-template <int G, int BLOCK = kGroupBlock>
+template <int G>
 struct GroupShape {
     static_assert(G == 4 || G == 16 || G == 64, "lanes per packet: a quad, a row or the wave");
-    static constexpr int P = BLOCK / G;                         // packets per workgroup
+    static constexpr int P = kGroupBlock / G;                   // packets per workgroup
     static constexpr int U = G == 64 ? 8 : G == 16 ? 6 : 2;     // loads per lane per trip
     static constexpr int R = G >= 16 ? G / 16 : 1;              // partial sums per packet
     static constexpr int S = P + 1;                             // LDS stride (odd: no conflicts)
@@ -309,20 +314,16 @@ struct GroupShape {
 };
 
 // ABL (profiling only, tools/wave_probe.hip): 1 = phase 2 stores the sum only.
-// LOCAL: each wave parses its own kWave / G packets (no workgroup barrier),
-// for BLOCK = 256: a small batch then spreads over every CU (4 096 packets
-// with G = 16: one wave per SIMD) and phase 2 runs on every SIMD at once.
-template <int MODE, bool RSS, int G, int ABL = 0, int BLOCK = kGroupBlock, bool LOCAL = false>
-__global__ __launch_bounds__(BLOCK) void rx_group_kernel(KParams kp) {
-    using Sh = GroupShape<G, BLOCK>;
+template <int MODE, bool RSS, int G, int ABL = 0>
+__global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
+    using Sh = GroupShape<G>;
     constexpr int P = Sh::P, U = Sh::U, R = Sh::R, S = Sh::S;
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ uint32_t hd[kHdRows * S];       // dword i of packet q at hd[i * S + q]
     __shared__ uint32_t psum[P * R];
     __shared__ uint4 info[P];                  // {p lo, p hi, L | ok << 16, nch}
     if constexpr (RSS) {
-        for (int i = threadIdx.x; i < kRssTableWords; i += BLOCK) rss_lds[i] = kp.rss_tables[i];
-        if constexpr (LOCAL) __syncthreads();
+        for (int i = threadIdx.x; i < kRssTableWords; i += kGroupBlock) rss_lds[i] = kp.rss_tables[i];
     }
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wib = threadIdx.x >> 6;
@@ -392,16 +393,11 @@ __global__ __launch_bounds__(BLOCK) void rx_group_kernel(KParams kp) {
         if ((lane & (kRow - 1)) == kRow - 1) psum[pkt * R + gl / kRow] = acc;
     }
     if (gl == 0) info[pkt] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), L | ((uint32_t)ok << 16), nch);
-    if constexpr (LOCAL) {
-        __builtin_amdgcn_wave_barrier();       // the wave's own packets: its LDS writes are in order
-    } else {
-        __syncthreads();
-    }
+    __syncthreads();
 
     // ---- phase 2: one lane per packet --------------------------------------------
-    if (!LOCAL && wib >= (uint32_t)Sh::W2) return;
-    if (LOCAL && lane >= (uint32_t)(kWave / G)) return;
-    const uint32_t q = LOCAL ? wib * (kWave / G) + lane : wib * kWave + lane;
+    if (wib >= (uint32_t)Sh::W2) return;
+    const uint32_t q = wib * kWave + lane;
     const uint32_t kk = blockIdx.x * P + q;
     if (q >= (uint32_t)P || kk >= kp.n) return;
     const uint4 inf = info[q];
