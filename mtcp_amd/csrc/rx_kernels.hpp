@@ -508,31 +508,33 @@ struct Trip {
 // STAMP (profiling builds, tools/rx_variants.hip): lane 0 of each wave writes
 // {start, end} of s_memrealtime (100 MHz), HW_REG_XCC_ID and HW_REG_HW_ID to
 // kp.stamps[4 * wave ...].
+// WPB: waves per workgroup (the grid then holds 8 / WPB workgroups per CU).
 // PRIO: the second workgroup on each CU (blockIdx >= gridDim / 2; the
 // dispatcher fills every CU once before the second round) runs at
 // s_setprio(PRIO & 3): the older wave of a SIMD otherwise wins its issue
 // arbitration and finishes first; PRIO & 4: only for the first half of its
 // passes.
 template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
-          bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
+          bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0,
+          int WPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
     uint64_t t_start = 0;
     if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
     if constexpr ((PRIO & 3) > 0) {
         if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(PRIO & 3);
     }
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
-    __shared__ WaveLds lds[kWavesPerBlock];
+    __shared__ WaveLds lds[WPB];
     if constexpr (RSS) {
-        for (int i = threadIdx.x; i < kRssTableWords; i += kBlock) rss_lds[i] = kp.rss_tables[i];
+        for (int i = threadIdx.x; i < kRssTableWords; i += kWave * WPB) rss_lds[i] = kp.rss_tables[i];
         __syncthreads();
     }
 
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t row = lane >> 4, rlane = lane & (kRow - 1);
     const uint32_t wib = threadIdx.x >> 6;
-    const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
-    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+    const uint32_t wave = blockIdx.x * WPB + wib;
+    const uint32_t nwaves = gridDim.x * WPB;
     WaveLds &wl = lds[wib];
     const uint32_t pass_pkts = nwaves * kWave;
     // packet index of lane l relative to the pass base

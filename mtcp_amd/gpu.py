@@ -9,6 +9,7 @@ return one verdict per packet in place of ProcessPacket's return value
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import numpy as np
@@ -43,7 +44,11 @@ def _dptr(t) -> int:
 
 
 class Context:
-    """One mtcp_gpu_ctx (one per mTCP thread; not re-entrant)."""
+    """One mtcp_gpu_ctx (one per mTCP thread; not re-entrant).
+
+    The `*_dev` methods take GPU tensors and a `stream`: a torch.cuda.Stream
+    or a raw hipStream_t handle; None (the default) orders the call after
+    the work PyTorch has queued on its current stream, as a torch op would."""
 
     def __init__(self, device: int = 0, rss: bool = False, rss_key: bytes | None = None,
                  rss_queues: int = 1, rss_endian: bool = True):
@@ -94,33 +99,57 @@ class Context:
         return lib().mtcp_gpu_dev_ioctl(self._h, nif, cmd, None)
 
     # -- device-resident ---------------------------------------------------
+    @contextlib.contextmanager
+    def _ordered(self, stream):
+        """The stream handle for one device call.  None: PyTorch's current
+        stream; when that is the legacy default stream, which the C-ABI
+        cannot name (NULL there means the context's own non-blocking
+        stream), the call is ordered by synchronizing before and after."""
+        if stream is not None:
+            yield _stream_handle(stream)
+            return
+        import torch
+        cur = torch.cuda.current_stream()
+        if cur.cuda_stream:
+            yield cur.cuda_stream
+            return
+        cur.synchronize()
+        yield None
+        torch.cuda.ExternalStream(lib().mtcp_gpu_stream(self._h)).synchronize()
+
     def rx_chunk_dev(self, buf, desc, n: int, off_shift: int, out, stream=None) -> None:
-        check(lib().mtcp_gpu_rx_chunk_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
-                                          _dptr(desc), n, off_shift, _dptr(out),
-                                          _stream_handle(stream)), "mtcp_gpu_rx_chunk_dev")
+        with self._ordered(stream) as st:
+            check(lib().mtcp_gpu_rx_chunk_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
+                                              _dptr(desc), n, off_shift, _dptr(out),
+                                              st), "mtcp_gpu_rx_chunk_dev")
 
     def rx_ptrs_dev(self, ptrs, lens, n: int, out, stream=None) -> None:
-        check(lib().mtcp_gpu_rx_ptrs_dev(self._h, _dptr(ptrs), _dptr(lens), n, _dptr(out),
-                                         _stream_handle(stream)), "mtcp_gpu_rx_ptrs_dev")
+        with self._ordered(stream) as st:
+            check(lib().mtcp_gpu_rx_ptrs_dev(self._h, _dptr(ptrs), _dptr(lens), n, _dptr(out),
+                                             st), "mtcp_gpu_rx_ptrs_dev")
 
     def rx_chunk_flow_dev(self, buf, desc, n: int, off_shift: int, out, bins, stream=None) -> None:
-        check(lib().mtcp_gpu_rx_chunk_flow_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
-                                               _dptr(desc), n, off_shift, _dptr(out), _dptr(bins),
-                                               _stream_handle(stream)), "mtcp_gpu_rx_chunk_flow_dev")
+        with self._ordered(stream) as st:
+            check(lib().mtcp_gpu_rx_chunk_flow_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
+                                                   _dptr(desc), n, off_shift, _dptr(out), _dptr(bins),
+                                                   st), "mtcp_gpu_rx_chunk_flow_dev")
 
     def rx_ptrs_flow_dev(self, ptrs, lens, n: int, out, bins, stream=None) -> None:
-        check(lib().mtcp_gpu_rx_ptrs_flow_dev(self._h, _dptr(ptrs), _dptr(lens), n, _dptr(out),
-                                              _dptr(bins), _stream_handle(stream)),
-              "mtcp_gpu_rx_ptrs_flow_dev")
+        with self._ordered(stream) as st:
+            check(lib().mtcp_gpu_rx_ptrs_flow_dev(self._h, _dptr(ptrs), _dptr(lens), n, _dptr(out),
+                                                  _dptr(bins), st),
+                  "mtcp_gpu_rx_ptrs_flow_dev")
 
     def tx_fill_ptrs_dev(self, ptrs, lens, n: int, stream=None) -> None:
-        check(lib().mtcp_gpu_tx_fill_ptrs_dev(self._h, _dptr(ptrs), _dptr(lens), n,
-                                              _stream_handle(stream)), "mtcp_gpu_tx_fill_ptrs_dev")
+        with self._ordered(stream) as st:
+            check(lib().mtcp_gpu_tx_fill_ptrs_dev(self._h, _dptr(ptrs), _dptr(lens), n,
+                                                  st), "mtcp_gpu_tx_fill_ptrs_dev")
 
     def tx_fill_dev(self, buf, desc, n: int, off_shift: int, stream=None) -> None:
-        check(lib().mtcp_gpu_tx_fill_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
-                                         _dptr(desc), n, off_shift, _stream_handle(stream)),
-              "mtcp_gpu_tx_fill_dev")
+        with self._ordered(stream) as st:
+            check(lib().mtcp_gpu_tx_fill_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
+                                             _dptr(desc), n, off_shift, st),
+                  "mtcp_gpu_tx_fill_dev")
 
     # -- host memory ---------------------------------------------------------
     def rx_chunk(self, buf: np.ndarray, desc: np.ndarray, off_shift: int = 0,
@@ -149,7 +178,6 @@ class Context:
                                      len(desc), off_shift, ctypes.byref(cnt)), "mtcp_gpu_tx_fill")
         return cnt.value
 
-
     def tx_fill_ptrs(self, buf: np.ndarray, offsets, lens) -> int:
         """mtcp_gpu_tx_fill_ptrs over frames of the host array `buf` at byte
         `offsets` (a DPDK-style pointer burst into one host buffer); fills
@@ -165,8 +193,9 @@ class Context:
 
     # -- flow-table hash (HashFlow, mtcp/src/tcp_stream.c:56-90) -------------
     def flow_hash_dev(self, res, n: int, bins, stream=None) -> None:
-        check(lib().mtcp_gpu_flow_hash_dev(self._h, _dptr(res), n, _dptr(bins),
-                                           _stream_handle(stream)), "mtcp_gpu_flow_hash_dev")
+        with self._ordered(stream) as st:
+            check(lib().mtcp_gpu_flow_hash_dev(self._h, _dptr(res), n, _dptr(bins),
+                                               st), "mtcp_gpu_flow_hash_dev")
 
     def flow_hash(self, res: np.ndarray) -> np.ndarray:
         res = np.ascontiguousarray(res, dtype=RESULT_DTYPE)
@@ -180,10 +209,11 @@ class Context:
                           num_queues: int, endian_check: bool, queue, stream=None) -> None:
         if queue.numel() * queue.element_size() < num_addr * (MAX_PORT - MIN_PORT):
             raise ValueError("queue buffer too small")
-        check(lib().mtcp_gpu_rss_queue_map_dev(self._h, saddr_base_h, num_addr, daddr_h, dport_h,
-                                               num_queues, int(endian_check), _dptr(queue),
-                                               _stream_handle(stream)),
-              "mtcp_gpu_rss_queue_map_dev")
+        with self._ordered(stream) as st:
+            check(lib().mtcp_gpu_rss_queue_map_dev(self._h, saddr_base_h, num_addr, daddr_h, dport_h,
+                                                   num_queues, int(endian_check), _dptr(queue),
+                                                   st),
+                  "mtcp_gpu_rss_queue_map_dev")
 
     def addr_pool_search(self, core: int, num_queues: int, saddr_base: int, num_addr: int,
                          daddr: int, dport: int, endian_check: bool = True,

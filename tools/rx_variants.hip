@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void wave_per_packet(mg::KParams kp) {
     }
 }
 
-struct Variant { const char *name; kfn fn; uint32_t blocks_per_cu; };
+struct Variant { const char *name; kfn fn; uint32_t blocks_per_cu; uint32_t wpb = 4; };
 
 static uint64_t mix(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -528,6 +528,8 @@ int main(int argc, char **argv) {
         // variant 0 = what mtcp_gpu.hip dispatches for C3; every other variant's
         // records must equal its records byte for byte
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
+        vs.push_back({"rss_sorted6_wpb8_cu1", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 8>, 1, 8});
+        vs.push_back({"rss_sorted6_wpb2_cu4", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 2>, 4, 2});
         vs.push_back({"rss_sorted6_prio1half_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 5>, 2});
         vs.push_back({"rss_sorted6_prio2half_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 6>, 2});
         vs.push_back({"rss_sorted6_prio1_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 1>, 2});
@@ -555,6 +557,9 @@ int main(int argc, char **argv) {
     } else {
         // variant 0 = what mtcp_gpu.hip dispatches for C2 (C5 adds LALIGN)
         vs.push_back({"unrolled_cu2", rx_kernel<kRxChunk, false, 3>, 2});
+        vs.push_back({"unrolled_wpb8_cu1", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 8>, 1, 8});
+        vs.push_back({"unrolled_wpb2_cu4", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 2>, 4, 2});
+        vs.push_back({"unrolled_lalign_rev_wpb8_cu1", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, false, 0, 8>, 1, 8});
         vs.push_back({"unrolled_prio1half_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 5>, 2});
         vs.push_back({"unrolled_prio2half_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 6>, 2});
         vs.push_back({"unrolled_lalign_rev_prio1half_cu2", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, false, 5>, 2});
@@ -602,6 +607,12 @@ int main(int argc, char **argv) {
         vs.push_back({"tx_unrolled_temporal_cu2", rx_kernel<kTxChunk, false, 3, false, 0, 8, 8, false>, 2});
     }
     if (single) vs.resize(1);
+    if (const char *only = getenv("RXV_ONLY")) {     // variant 0 and the named ones
+        std::vector<Variant> keep{vs[0]};
+        for (size_t v = 1; v < vs.size(); ++v)
+            if (strstr(only, vs[v].name)) keep.push_back(vs[v]);
+        vs = keep;
+    }
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
@@ -611,13 +622,13 @@ int main(int argc, char **argv) {
     const int reps = 20;
     for (int r = 0; r < rounds; ++r) {
         for (size_t v = 0; v < vs.size(); ++v) {
-            const uint32_t groups = (n + 63) / 64;
+            const uint32_t groups = (n + 63) / 64, wpb = vs[v].wpb;
             uint32_t blocks = strstr(vs[v].name, "plain") ? 1u << 20
-                              : strstr(vs[v].name, "wpp") ? (n + 3) / 4 : (groups + 3) / 4;
+                              : strstr(vs[v].name, "wpp") ? (n + 3) / 4 : (groups + wpb - 1) / wpb;
             if (blocks > cus * vs[v].blocks_per_cu) blocks = cus * vs[v].blocks_per_cu;
             kp.out = v == 0 ? d_ref : d_out;
             CK(hipMemset(kp.out, 0, n * sizeof(mtcp_gpu_result)));
-            const uint32_t threads = 256;
+            const uint32_t threads = 64 * wpb;
             hipLaunchKernelGGL(vs[v].fn, dim3(blocks), dim3(threads), 0, 0, kp);
             CK(hipEventRecord(a));
             for (int i = 0; i < reps; ++i)
