@@ -22,6 +22,11 @@
 #include "../../include/mtcp_gpu_rxq.h"
 #include "host_copy.hpp"
 
+// get_rptr serves frame i; the header of frame i + kServeAhead is fetched
+// meanwhile (the staged frames were written with streaming stores, so each
+// header is a DRAM read, at a 1.5 KiB stride for MTU frames)
+constexpr uint32_t kServeAhead = 16;
+
 struct mtcp_gpu_rxq {
     mtcp_gpu_ctx *ctx = nullptr;
     int device = 0;
@@ -38,7 +43,25 @@ struct mtcp_gpu_rxq {
     uint32_t done_n = 0;                 // frames with results
     uint32_t inflight = 0;               // frames of an unfinished flush_async (0: none)
     uint64_t used = 0;                   // staging bytes in use
+    // A/B knobs (environment at create): MTCP_GPU_STAGE=plain copies frames
+    // with memcpy (cached stores) instead of streaming stores;
+    // MTCP_GPU_SERVE_AHEAD=k prefetches frame i + k's header and result when
+    // frame i is served (0: off)
+    bool plain = false;
+    uint32_t ahead = kServeAhead;
+    uint32_t hint = 3;                   // MTCP_GPU_SERVE_HINT: prefetch locality 0..3
 };
+
+namespace {
+inline void serve_prefetch(const void *p, uint32_t hint) {
+    switch (hint) {
+    case 0: __builtin_prefetch(p, 0, 0); break;
+    case 1: __builtin_prefetch(p, 0, 1); break;
+    case 2: __builtin_prefetch(p, 0, 2); break;
+    default: __builtin_prefetch(p, 0, 3); break;
+    }
+}
+}  // namespace
 
 namespace {
 
@@ -76,6 +99,9 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     q->max_pkts = max_pkts;
     q->max_bytes = (max_bytes + 63) & ~63ull;
     q->stream = reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx));
+    if (const char *e = getenv("MTCP_GPU_STAGE")) q->plain = strcmp(e, "plain") == 0;
+    if (const char *e = getenv("MTCP_GPU_SERVE_AHEAD")) q->ahead = (uint32_t)atoi(e);
+    if (const char *e = getenv("MTCP_GPU_SERVE_HINT")) q->hint = (uint32_t)atoi(e);
     const uint64_t staging = q->max_bytes + (uint64_t)max_pkts * sizeof(mtcp_gpu_desc);
     if (hipEventCreateWithFlags(&q->evt, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&q->buf, staging, hipHostMallocDefault) != hipSuccess ||
@@ -134,7 +160,10 @@ int mtcp_gpu_rxq_push(mtcp_gpu_rxq *q, const uint8_t *frame, uint16_t len) {
     d.offset = (uint32_t)(q->used >> 6);           // 64 B units (off_shift 6)
     d.len = len;
     d.flags = d.rsvd = 0;
-    if (len) stage_copy(q->buf + q->used, frame, len);
+    if (len) {
+        if (q->plain) memcpy(q->buf + q->used, frame, len);
+        else stage_copy(q->buf + q->used, frame, len);
+    }
     q->used += slot;
     q->n++;
     return MTCP_GPU_OK;
@@ -212,6 +241,10 @@ int mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n) {
 uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
                           const mtcp_gpu_result **res) {
     if (!q || i >= q->done_n) return nullptr;
+    if (q->ahead && i + q->ahead < q->done_n) {
+        serve_prefetch(q->buf + ((uint64_t)q->desc[i + q->ahead].offset << 6), q->hint);
+        serve_prefetch(&q->res[i + q->ahead], q->hint);
+    }
     const mtcp_gpu_result &r = q->res[i];
     if (len) *len = q->desc[i].len;
     if (res) *res = &r;
@@ -226,6 +259,8 @@ uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
 
 uint8_t *mtcp_gpu_rxq_frame(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len) {
     if (!q || i >= q->n) return nullptr;
+    if (q->ahead && i + q->ahead < q->n)
+        serve_prefetch(q->buf + ((uint64_t)q->desc[i + q->ahead].offset << 6), q->hint);
     if (len) *len = q->desc[i].len;
     return q->buf + ((uint64_t)q->desc[i].offset << 6);
 }

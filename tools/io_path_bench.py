@@ -122,6 +122,28 @@ def main():
         seeds = {64: 1, 1500: 2, "bimodal": 3}
         dump(n, size, seeds.get(size, 7), sys.argv[3])
         return
+    if "--quick" in sys.argv:
+        # A/B of the staging knobs (rxq.hip): 1 thread, 1500 B, timing and verify
+        with tempfile.TemporaryDirectory() as tmp:
+            sweep = [{"MTCP_GPU_SERVE_AHEAD": str(a)} for _ in range(3) for a in (0, 16)]
+            for knobs in sweep:
+                os.environ.pop("MTCP_GPU_STAGE", None)
+                os.environ.pop("MTCP_GPU_SERVE_AHEAD", None)
+                os.environ.update(knobs)
+                for mode in ("timing", "verify"):
+                    r = run(n, 1500, 2, tmp, mode, 1, True)
+                    print(json.dumps({"knobs": knobs, "mode": mode, "mpkt_per_s": r["mpkt_per_s"],
+                                      "GBs": r["GBs"]}), flush=True)
+            for knobs in ({"MTCP_GPU_SERVE_AHEAD": "0"}, {"MTCP_GPU_SERVE_AHEAD": "16"}):
+                os.environ.update(knobs)
+                for threads in (4, 8):
+                    r = run(n, 1500, 2, tmp, "timing", threads, True)
+                    print(json.dumps({"knobs": knobs, "threads": threads, "mpkt_per_s": r["mpkt_per_s"]}),
+                          flush=True)
+            ref = reference(n, 1500, 2)
+            if ref:
+                print(json.dumps(ref), flush=True)
+        return
     with tempfile.TemporaryDirectory() as tmp:
         for size, seed in ((1500, 2), (64, 1), ("bimodal", 3)):
             for mode, pipeline in (("timing", True), ("timing", False), ("verify", True)):
