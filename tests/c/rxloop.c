@@ -211,11 +211,24 @@ static void *worker_main(void *arg)
             const mtcp_gpu_desc *d = &f->desc[w->seen + (uint32_t)i];
             if (pktbuf != NULL) {
                 /* ProcessPacket(mtcp, rx_inf, ts, pktbuf, len) would run here */
-                if (w->timing) {
+                if (w->timing == 1) {
                     /* timing mode: touch the headers as ProcessPacket's parse
                      * would (first 64 B), no byte-for-byte check */
                     uint32_t k;
                     for (k = 0; k < 64 && k < len; k += 8) w->hdr_sum += pktbuf[k];
+                    w->status[w->seen + i] = 1;
+                } else if (w->timing == 2) {
+                    /* payload mode: read every byte once, as the payload's copy
+                     * into the stream's receive buffer would (tcp_in.c ->
+                     * RBPut), no byte-for-byte check */
+                    uint64_t acc = 0;
+                    uint32_t k;
+                    for (k = 0; k + 8 <= len; k += 8) {
+                        uint64_t v;
+                        memcpy(&v, pktbuf + k, 8);
+                        acc += v;
+                    }
+                    w->hdr_sum += acc;
                     w->status[w->seen + i] = 1;
                 } else {
                     int same = len == d->len && memcmp(pktbuf, f->buf + d->offset, len) == 0;
@@ -253,10 +266,11 @@ int main(int argc, char **argv)
     FILE *out;
 
     if (argc < 4) {
-        fprintf(stderr, "usage: rxloop CHUNK DESC OUT [timing|verify] [THREADS]\n");
+        fprintf(stderr, "usage: rxloop CHUNK DESC OUT [timing|payload|verify|tx] [THREADS]\n");
         return 1;
     }
-    timing = argc > 4 && strcmp(argv[4], "timing") == 0;
+    timing = argc > 4 && strcmp(argv[4], "timing") == 0 ? 1
+             : argc > 4 && strcmp(argv[4], "payload") == 0 ? 2 : 0;
     int tx = argc > 4 && strcmp(argv[4], "tx") == 0;
     uint8_t *tx_buf = NULL;
     threads = argc > 5 ? atoi(argv[5]) : 1;

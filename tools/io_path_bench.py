@@ -98,8 +98,10 @@ def run(n, size, seed, tmp, mode, threads=1, pipeline=True, tx=True):
             "note": "each mTCP thread: copy into pinned staging + one H2D (frames + descriptors) + "
                     "rx kernel + D2H per 4096 frames, get_rptr from staging; pipelined: aggregate "
                     "k served while k+1 is on the GPU; mode timing: the first 64 B of each served "
-                    "frame read (as ProcessPacket's parse would), mode verify: every served frame "
-                    "compared with the original; wall clock of the rx loop, best of 3"}
+                    "frame read (as ProcessPacket's parse would), mode payload: every byte of it "
+                    "read once (as the payload's copy into the receive buffer would), mode verify: "
+                    "every served frame compared with the original (a correctness mode, two "
+                    "streams); wall clock of the rx loop, best of 3"}
 
 
 def dump(n, size, seed, out_dir):
@@ -125,16 +127,16 @@ def main():
     if "--quick" in sys.argv:
         # A/B of the staging knobs (rxq.hip): 1 thread, 1500 B, timing and verify
         with tempfile.TemporaryDirectory() as tmp:
-            sweep = [{"MTCP_GPU_SERVE_AHEAD": str(a)} for _ in range(3) for a in (0, 16)]
+            sweep = [{"MTCP_GPU_STAGE": st} for _ in range(3) for st in ("nt", "plain")]
             for knobs in sweep:
                 os.environ.pop("MTCP_GPU_STAGE", None)
                 os.environ.pop("MTCP_GPU_SERVE_AHEAD", None)
                 os.environ.update(knobs)
-                for mode in ("timing", "verify"):
+                for mode in ("timing", "payload"):
                     r = run(n, 1500, 2, tmp, mode, 1, True)
                     print(json.dumps({"knobs": knobs, "mode": mode, "mpkt_per_s": r["mpkt_per_s"],
                                       "GBs": r["GBs"]}), flush=True)
-            for knobs in ({"MTCP_GPU_SERVE_AHEAD": "0"}, {"MTCP_GPU_SERVE_AHEAD": "16"}):
+            for knobs in ({"MTCP_GPU_STAGE": "nt"}, {"MTCP_GPU_STAGE": "plain"}):
                 os.environ.update(knobs)
                 for threads in (4, 8):
                     r = run(n, 1500, 2, tmp, "timing", threads, True)
@@ -146,7 +148,7 @@ def main():
         return
     with tempfile.TemporaryDirectory() as tmp:
         for size, seed in ((1500, 2), (64, 1), ("bimodal", 3)):
-            for mode, pipeline in (("timing", True), ("timing", False), ("verify", True)):
+            for mode, pipeline in (("timing", True), ("payload", True), ("timing", False), ("verify", True)):
                 print(json.dumps(run(n, size, seed, tmp, mode, 1, pipeline)), flush=True)
         for size, seed in ((1500, 2), (64, 1)):
             for threads in (2, 4, 8, 16):
