@@ -48,8 +48,9 @@ int main(int argc, char **argv) {
         {"seg0", mg::rx_wave_kernel<mg::kRxChunk, false, 0, 0>, 256, 4},
         {"nl2", mg::rx_wave_kernel<mg::kRxChunk, false, 0, 1, 2>, 256, 4},
         {"nl4", mg::rx_wave_kernel<mg::kRxChunk, false, 0, 1, 4>, 256, 4},
-        {"head", mg::rx_wave_kernel<mg::kRxChunk, false, 3>, 256, 4},
-        {"segsum", mg::rx_wave_kernel<mg::kRxChunk, false, 4>, 256, 4},
+        {"head", mg::rx_wave_kernel<mg::kRxChunk, false, 3, 1, 2>, 256, 4},
+        {"segsum", mg::rx_wave_kernel<mg::kRxChunk, false, 4, 1, 2>, 256, 4},
+        {"p1nl2", mg::rx_wave_kernel<mg::kRxChunk, false, 1, 1, 2>, 256, 4},
         {"g64_p1", mg::rx_group_kernel<mg::kRxChunk, false, 64, 1>, 1024, 16},
         {"g64", mg::rx_group_kernel<mg::kRxChunk, false, 64>, 1024, 16},
         {"g16_p1", mg::rx_group_kernel<mg::kRxChunk, false, 16, 1>, 1024, 64},
@@ -106,12 +107,13 @@ int main(int argc, char **argv) {
             // every full variant's records must equal the wave kernel's
             static std::vector<mtcp_gpu_result> ref;
             const bool full = !strchr(v.name, '_') && strcmp(v.name, "empty") && strcmp(v.name, "desc") &&
-                              strcmp(v.name, "phase1") && strcmp(v.name, "head") && strcmp(v.name, "segsum");
+                              strcmp(v.name, "phase1") && strcmp(v.name, "head") && strcmp(v.name, "segsum") &&
+                              strcmp(v.name, "p1nl2");
             if (full) {
                 std::vector<mtcp_gpu_result> got(n);
                 CK(hipMemcpy(got.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 if (!strcmp(v.name, "full")) ref = got;
-                else if (memcmp(ref.data(), got.data(), n * sizeof(mtcp_gpu_result)) != 0) {
+                else if (ref.size() == n && memcmp(ref.data(), got.data(), n * sizeof(mtcp_gpu_result)) != 0) {
                     fprintf(stderr, "%s records differ from the wave kernel's (n %u)\n", v.name, n);
                     return 2;
                 }
