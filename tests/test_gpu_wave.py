@@ -22,7 +22,8 @@ import numpy as np
 import pytest
 
 import oracle
-from mtcp_amd import RESULT_DTYPE, pktgen
+from mtcp_amd import DESC_DTYPE, RESULT_DTYPE, pktgen
+from tests.fuzz_frames import fuzz_batch
 from tests.golden_io import compare_results
 from tests.repack import repack
 from tests.test_gpu_parity import DEV, assert_same, dev_results, run_rx_dev, to_dev
@@ -100,6 +101,41 @@ def test_small_batches_every_schedule(gpu, monkeypatch, n, size, rss):
         with ctx_for(gpu, monkeypatch, sched, **kw) as ctx:
             assert_same(run_rx_dev(ctx, buf, desc, 6), want, f"{sched} {size} x {n}")
     assert (want["verdict"] == 0).mean() > 0.99
+
+
+def test_short_trip_kernel_with_jumbo_frames(gpu, monkeypatch):
+    """A batch whose average slot is at most 2 KiB takes the wave kernel's
+    2-load trips (mtcp_gpu.hip kWaveShortUpToSlot): its jumbo frames then
+    need several trips and the masked segment sum; with the fuzz frames'
+    padded and truncated datagrams spliced in, every kernel equals the
+    oracle, chunk and pointer modes."""
+    rng = np.random.default_rng(71)
+    n = 4096
+    lens = np.where(rng.random(n) < .06, rng.integers(2049, 16001, n),
+                    np.where(rng.random(n) < .5, 1500, rng.integers(54, 1400, n))).astype(np.uint16)
+    desc, nbytes = pktgen.layout_from_lengths(lens, 6)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, 71, 0)
+    fb, fd = fuzz_batch(512, 72, True)                # padded / truncated datagrams, 64 B slots
+    base = nbytes
+    buf = np.concatenate([buf, fb])
+    fd = fd.copy()
+    fd["offset"] = (fd["offset"] >> 6) + (base >> 6)     # byte offsets -> 64 B units
+    desc = np.concatenate([desc, fd])
+    assert buf.nbytes // len(desc) <= 2048
+    want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(None, 8, 1))
+    assert (want["verdict"] == 0).sum() > 3000
+    for sched in SCHEDS:
+        with ctx_for(gpu, monkeypatch, sched, rss=True, rss_queues=8, rss_endian=True) as ctx:
+            assert_same(run_rx_dev(ctx, buf, desc, 6), want, f"{sched} short trips, chunk")
+            b = to_dev(buf)
+            bdesc = desc.copy()
+            bdesc["offset"] = desc["offset"] << 6
+            ptrs, lns = ptr_burst(b, bdesc)
+            out = dev_results(len(desc))
+            ctx.rx_ptrs_dev(ptrs, lns, len(desc), out)
+            torch.cuda.synchronize()
+            assert_same(out.cpu().numpy().view(RESULT_DTYPE), want, f"{sched} short trips, pointers")
 
 
 @pytest.mark.parametrize("key,nq,endian", [(None, 8, 1), ("ms", 16, 0), ("ms", 5, 1)])
