@@ -133,6 +133,14 @@ __global__ __launch_bounds__(256) void slot_scatter(uint8_t *buf, uint32_t nslot
         if (WIDE == 0) {
             reinterpret_cast<uint16_t *>(f)[12] = (uint16_t)(s ^ salt);
             reinterpret_cast<uint16_t *>(f)[25] = (uint16_t)(s + salt);
+        } else if (WIDE == 3) {                      // read the 64 B, patch, write it whole
+            v4u w[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) w[c] = reinterpret_cast<const v4u *>(f)[c];
+            w[1].z = (w[1].z & 0xFFFF0000u) | (s & 0xFFFFu);
+            w[3].x = (w[3].x & 0x0000FFFFu) | (salt << 16);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) reinterpret_cast<v4u *>(f)[c] = w[c];
         } else {
             const v4u w = {s, salt, s ^ salt, 5u};
 #pragma unroll
@@ -216,6 +224,11 @@ int main() {
                                       slot_scatter<2><<<(ns + 255) / 256, 256>>>(sb, ns, 3); }, 20);
         const float q4 = timeit([&] { slot_patch<0><<<blocks, 256>>>(sb, ns);
                                       slot_scatter<1><<<(ns + 255) / 256, 256>>>(sb, ns, 3); }, 20);
+        const float q5 = timeit([&] { slot_patch<0><<<blocks, 256>>>(sb, ns);
+                                      slot_scatter<3><<<(ns + 255) / 256, 256>>>(sb, ns, 3); }, 20);
+        const float q6 = timeit([&] { slot_scatter<3><<<(ns + 255) / 256, 256>>>(sb, ns, 3); }, 20);
+        printf("{\"probe\": \"slot_rmw\", \"read_then_scatter_rmw64_us\": %.2f, \"scatter_rmw64_alone_us\": %.2f}\n",
+               q5, q6);
         const float p7 = timeit([&] { slot_patch<7><<<blocks, 256>>>(sb, ns); }, 20);
         const float p8 = timeit([&] { slot_patch<8><<<blocks, 256>>>(sb, ns); }, 20);
         const float p9 = timeit([&] { slot_patch<9><<<blocks, 256>>>(sb, ns); }, 20);
