@@ -82,6 +82,8 @@ def parse():
                     help="packets in the CPU sample (default: the whole 1-GPU batch, "
                          "larger than the host L3, so the CPU streams from DRAM like the GPU)")
     ap.add_argument("--pcie", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--small-batch", default="on", choices=["on", "off"],
+                    help="N=1: also time one 4 096-frame aggregate (graph-captured launches)")
     ap.add_argument("--pcie-max-bytes", type=int, default=1 << 30,
                     help="frame bytes per rank in the PCIe-inclusive leg (a prefix of the "
                          "shard, staged to host memory piece by piece)")
@@ -203,6 +205,44 @@ def pcie_inclusive(ctx, host_buf, desc, nbytes, world):
             "note": "pinned host chunk in, host results out; H2D + kernel + D2H overlapped "
                     "on 3 streams, 64 MiB stages; each rank its shard's first frames (at most "
                     "--pcie-max-bytes), all ranks at once, wall clock max over ranks, best of 3"}
+
+
+def small_batch(ctx, dev, stream, n=4096, size=1500, launches=100, reps=5):
+    """One io_module aggregate (4 096 x 1500 B frames, the batch the
+    io_module backend launches; mTCP's bursts are <= 64 frames,
+    dpdk_module.c:71) through mtcp_gpu_rx_chunk_dev: `launches` back-to-back
+    launches captured in one HIP graph, so that the per-launch time is the
+    kernel's and not the Python call's; median over `reps` replays."""
+    from mtcp_amd import gpu
+    desc, nbytes = pktgen.layout(n, size, 6, 7)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+    o = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+    gpu.pktgen_dev(b, d, n, 6, 7, stream=stream)
+    for _ in range(5):
+        ctx.rx_chunk_dev(b, d, n, 6, o, stream=stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        for _ in range(launches):
+            ctx.rx_chunk_dev(b, d, n, 6, o, stream=stream)
+    g.replay()
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1) * 1e3 / launches)
+    us = sorted(times)[len(times) // 2]
+    frame_bytes = int(desc["len"].astype(np.int64).sum())
+    return {"frames": n, "frame_size": size, "us_per_launch": round(us, 2),
+            "GBs": round(frame_bytes / us / 1e3, 1), "gpkt_per_s": round(n / us / 1e3, 3),
+            "kernel": "mg::rx_wave_kernel (a wavefront per packet, 2-load trips)",
+            "note": f"{launches} launches of mtcp_gpu_rx_chunk_dev captured in a HIP graph, "
+                    f"HIP events over a replay, median of {reps}"}
 
 
 def _timed(step, steps, warmup, stream):
@@ -453,6 +493,11 @@ def main():
         except Exception as exc:   # report, never fake
             extra["cpu_baseline"] = {"value": None, "error": repr(exc)}
         del host
+    if rank == 0 and world == 1 and args.small_batch != "off":
+        try:
+            extra["small_batch"] = small_batch(ctx, dev, stream)
+        except Exception as exc:      # never costs the headline line
+            extra["small_batch"] = {"error": repr(exc)}
     if want_pcie:
         host, hdesc = host_prefix(d_buf, sh.desc, max_bytes=args.pcie_max_bytes)
         extra["pcie_inclusive"] = pcie_inclusive(ctx, host, hdesc,
