@@ -219,13 +219,17 @@ struct Pkt {
 // the bytes each step has checked to lie inside the frame (L bytes);
 // ipsum(ihl) = the sum of the 16-bit words of the IP header, bytes
 // [14, 14 + 4*ihl), for 5 <= ihl <= 15 (ip_fast_csum's adc chain, exact:
-// SURVEY §8 a2').
-template <int MODE, class PD, class IPSUM>
-__device__ __forceinline__ Pkt parse_head(PD pd, IPSUM ipsum, uint32_t L, bool desc_ok) {
+// SURVEY §8 a2'); sw(i) = bytes 4i+2..4i+5 (the funnel of dwords i and i+1
+// by 16 bits: every 4-byte field past the Ethernet header sits there) and
+// swb(i) = its byte swap — a wave parsing one packet computes both in all
+// lanes at once and reads them out, instead of two shifts and an or per field.
+template <int MODE, class PD, class IPSUM, class SW, class SWB>
+__device__ __forceinline__ Pkt parse_head(PD pd, IPSUM ipsum, SW sw, SWB swb, uint32_t L,
+                                          bool desc_ok) {
     Pkt k;
-    uint32_t h[9];
+    uint32_t h[7];
 #pragma unroll
-    for (int i = 3; i < 9; ++i) h[i] = pd(i);
+    for (int i = 3; i < 7; ++i) h[i] = pd(i);
     const uint32_t d0 = h[3];                 // bytes 12..15
     if (!desc_ok) return k;
     k.verdict = MTCP_GPU_V_TRUNCATED;
@@ -279,16 +283,15 @@ __device__ __forceinline__ Pkt parse_head(PD pd, IPSUM ipsum, uint32_t L, bool d
     }
     if (tcp_entry) {
         // tcp_in.c:1142-1149: tcph = iph + 4*ihl
-        const uint32_t tw = (k.T - 2) >> 2;
-        const uint32_t e0 = pd(tw), e1 = pd(tw + 1), e2 = pd(tw + 2);
+        const uint32_t tw = (k.T - 2) >> 2;                                // T = 4 tw + 2
         const uint32_t e3 = pd(tw + 3), e4 = pd(tw + 4);
         const uint32_t doff = (e3 >> 20) & 0xFu;
         k.tcp_entry = true;
-        k.saddr = (h[6] >> 16) | (h[7] << 16);
-        k.daddr = (h[7] >> 16) | (h[8] << 16);
-        k.ports = (e0 >> 16) | (e1 << 16);                                 // sport | dport << 16
-        k.seq = bswap32((e1 >> 16) | (e2 << 16));
-        k.ack = bswap32((e2 >> 16) | (e3 << 16));
+        k.saddr = sw(6);                                                   // bytes 26..29
+        k.daddr = sw(7);                                                   // bytes 30..33
+        k.ports = sw(tw);                                                  // sport | dport << 16
+        k.seq = swb(tw + 1);
+        k.ack = swb(tw + 2);
         k.window = bswap16(e4 & 0xFFFFu);
         k.flags = e3 >> 24;
         k.tcheck = e4 >> 16;
@@ -359,7 +362,9 @@ __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, u
         }
         return s_ip + lo_last;
     };
-    Pkt k = parse_head<MODE>(pd, ipsum, L, desc_ok);
+    auto sw = [&](uint32_t i) -> uint32_t { return __builtin_amdgcn_alignbit(pd(i + 1), pd(i), 16); };
+    auto swb = [&](uint32_t i) -> uint32_t { return bswap32(sw(i)); };
+    Pkt k = parse_head<MODE>(pd, ipsum, sw, swb, L, desc_ok);
     if (k.need_sum) {
         // The chunk sum covers [p16, p16 + 16*nch).  Remove the bytes before
         // the frame, the header bytes [0, T), and everything at or past

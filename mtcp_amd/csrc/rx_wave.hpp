@@ -171,13 +171,21 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
     auto ipsum = [&](uint32_t ihl) -> uint32_t {
         // words of bytes [14, 14 + 4*ihl): the high half of dword 3, dwords
         // 4 .. 2 + ihl, the low half of dword 3 + ihl
-        const uint32_t w = lane == 3 ? pdw >> 16
-                           : lane > 3 && lane < 3 + ihl ? (pdw & 0xFFFFu) + (pdw >> 16)
-                           : lane == 3 + ihl ? pdw & 0xFFFFu : 0u;
+        // (as lane masks, not branches: the scalar unit is this kernel's bound)
+        const uint32_t hi = pdw >> 16, lo = pdw & 0xFFFFu;
+        const uint32_t m3 = 0u - (uint32_t)(lane == 3);
+        const uint32_t mm = 0u - (uint32_t)(lane > 3 && lane < 3 + ihl);
+        const uint32_t ml = 0u - (uint32_t)(lane == 3 + ihl);
+        const uint32_t w = (hi & (m3 | mm)) + (lo & (mm | ml));
         const uint32_t r = row_sum(w);
         return (uint32_t)__builtin_amdgcn_readlane((int)r, 15) + (uint32_t)__builtin_amdgcn_readlane((int)r, 31);
     };
-    Pkt pk = parse_head<MODE>(pd, ipsum, L, ok);
+    // bytes 4i+2..4i+5 in lane i (lane i + 1's dword through DPP wave_shl:1)
+    const uint32_t nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pdw, 0x130, 0xF, 0xF, false);
+    const uint32_t swv = __builtin_amdgcn_alignbit(nxt, pdw, 16), swbv = bswap32(swv);
+    auto sw = [&](uint32_t i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)swv, (int)i); };
+    auto swb = [&](uint32_t i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)swbv, (int)i); };
+    Pkt pk = parse_head<MODE>(pd, ipsum, sw, swb, L, ok);
     if constexpr (ABL == 3) {
         if (lane == 0) kp.out[k].saddr = pk.verdict;
         return;
@@ -195,16 +203,19 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
         // mid-dword) and [E, 16 * nch) from the last chunk, by its lane
         const uint32_t nb = sh + pk.T, whole = nb >> 2, te = e_rel & 15;
         const uint32_t v = hd[lane < 23 ? lane : 0u];
-        uint32_t w = lane < whole ? halves(v, 0u) : (lane == whole && (nb & 2)) ? (v & 0xFFFFu) : 0u;
+        const uint32_t mw = 0u - (uint32_t)(lane < whole);
+        const uint32_t mh = 0u - (uint32_t)(lane == whole && (nb & 2));
+        uint32_t w = halves(v & mw, 0u) + (v & 0xFFFFu & mh);
         const uint32_t d[4] = {last.x, last.y, last.z, last.w};
         uint32_t t = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int drop = (int)te - 4 * j;                            // low bytes inside the segment
-            const uint32_t m = drop <= 0 ? 0xFFFFFFFFu : drop >= 4 ? 0u : (0xFFFFFFFFu << (8 * drop));
-            t = halves(d[j] & m, t);
+            // bytes of dword j at or past E: all when E lies before it, none
+            // when after it, else its bytes from E - 4j on
+            const int sft = min(max(8 * ((int)te - 4 * j), 0), 32);
+            t = halves(d[j] & (uint32_t)(0xFFFFFFFFull << sft), t);
         }
-        w += (te && lane == (nch - 1) % kWave) ? t : 0u;
+        w += t & (0u - (uint32_t)(te && lane == (nch - 1) % kWave));
         acc -= w;
         acc = row_sum(acc);
         const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)acc, 15) +
