@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256) void wave_per_packet(mg::KParams kp) {
 // flight per lane), in run order, so the grid reads one compact window at a
 // time and every 128 B line of a run, small frames' included, exactly once,
 // in order.  No per-frame attribution: a ceiling for that schedule.
-template <int U>
+template <int U, bool SKIP = false>
 __global__ __launch_bounds__(256) void run_stream(mg::KParams kp) {
     using namespace mg;
     const uint32_t lane = threadIdx.x & 63;
@@ -371,7 +371,9 @@ __global__ __launch_bounds__(256) void run_stream(mg::KParams kp) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t c = c0 + u * 64 + lane;
-                    x[u] = gload_nt(rlo + 16ull * (c < nc ? c : nc - 1));
+                    // SKIP: no load instruction for a window wholly past the run
+                    if (!SKIP || c0 + u * 64 < nc) x[u] = gload_nt(rlo + 16ull * (c < nc ? c : nc - 1));
+                    else x[u] = v4u{0, 0, 0, 0};
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) acc += (c0 + u * 64 + lane < nc) ? halves4(x[u], 0u) : 0u;
@@ -604,6 +606,10 @@ int main(int argc, char **argv) {
         vs.push_back({"runstream8_cu2", run_stream<8>, 2});
         vs.push_back({"runstream12_cu2", run_stream<12>, 2});
         vs.push_back({"runstream16_cu2", run_stream<16>, 2});
+        vs.push_back({"runstream12skip_cu2", run_stream<12, true>, 2});
+        vs.push_back({"runstream16skip_cu2", run_stream<16, true>, 2});
+        vs.push_back({"runstream24skip_cu2", run_stream<24, true>, 2});
+
         vs.push_back({"abl1_rss_sorted6_nostore_u8_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 8, true, 8>, 2});
         vs.push_back({"rss_sorted6_u8_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 8>, 2});
         vs.push_back({"rss_sorted6_u8_defer4_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 4, 8, true, 8>, 2});
