@@ -28,7 +28,6 @@ frames copied to host memory.
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import os
 import time
@@ -37,7 +36,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from mtcp_amd import pktgen, shard
+from mtcp_amd import _codeobj, pktgen, shard
 
 METRIC = "device-resident Gpkt/s + payload GB/s checksummed, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -123,10 +122,11 @@ def host_prefix(d_buf, desc, max_pkts=None, max_bytes=None):
 
 def lib_sha256() -> str:
     """Identity of the product library whose kernels this run measures: the
-    committed PMC traffic figure (profiles/traffic_*.json) counts only when it
-    was collected on the same build."""
+    committed PMC traffic figure (profiles/traffic_*.json) counts when it was
+    collected on the same build, or on one whose rx_kernel sources are the
+    same (mtcp_amd/_codeobj.py)."""
     from mtcp_amd import _lib
-    return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+    return _codeobj.lib_sha256(_lib.LIB_PATH)
 
 
 def cpu_share() -> int:
@@ -517,6 +517,10 @@ def main():
             if tj.get("lib_sha256") == lib_sha256():
                 traffic = tj.get("hbm_bytes_per_launch")
                 traffic_note = f"rocprofv3 PMC of this build ({os.path.relpath(tpath)})"
+            elif tj.get("rx_source_key") == _codeobj.rx_source_key():
+                traffic = tj.get("hbm_bytes_per_launch")
+                traffic_note = (f"rocprofv3 PMC of a build with the same rx_kernel sources "
+                                f"({os.path.relpath(tpath)}; the library differs elsewhere)")
             else:
                 traffic_note = (f"stale: {os.path.relpath(tpath)} was collected on another build "
                                 f"({tj.get('hbm_bytes_per_launch')} B per launch there)")

@@ -7,6 +7,7 @@
 cfg=$1; out=$2
 mkdir -p "$out"
 sha256sum mtcp_amd/lib/libmtcp_gpu.so | cut -d' ' -f1 > "$out/lib.sha256"   # the build profiled
+python3 -c "from mtcp_amd import _codeobj; print(_codeobj.rx_source_key())" > "$out/rx_source.key"
 b="python3 bench.py --config $cfg --steps 200 --warmup 20 --cpu-baseline off --pcie off"
 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$out/trace" -o run -- $b > "$out/trace.log" 2>&1 || exit $?
 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$out/fetch" -o run -- $b > "$out/fetch.log" 2>&1 || exit $?

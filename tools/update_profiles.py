@@ -30,8 +30,9 @@ for c in cfgs:
     s = json.load(open(summ))
     json.dump({
         "config": c,
-        # bench.py uses the figure only on this same build (bench.lib_sha256)
+        # bench.py uses the figure on this build or one with the same rx_kernel sources (mtcp_amd/_codeobj.py)
         "lib_sha256": open(os.path.join(src, "lib.sha256")).read().strip(),
+        "rx_source_key": open(os.path.join(src, "rx_source.key")).read().strip(),
         "hbm_bytes_per_launch": s["hbm_bytes_per_launch"],
         "hbm_read_bytes_per_launch": s["hbm_read_bytes_per_launch"],
         "hbm_write_bytes_per_launch": s["hbm_write_bytes_per_launch"],
