@@ -365,7 +365,9 @@ static void finish(struct gpu_private_context *g, struct gpu_ifq *f, int a)
     f->served_raw[a] = 1;
     if (!f->launched[a])
         return;
-    if (mtcp_gpu_rxq_wait(f->rxq[a], &n_done) == MTCP_GPU_OK && n_done == f->count[a] && g->gpu)
+    if (!g->gpu)
+        return;                       /* failed meanwhile: gpu_fail already waited */
+    if (mtcp_gpu_rxq_wait(f->rxq[a], &n_done) == MTCP_GPU_OK && n_done == f->count[a])
         f->served_raw[a] = 0;
     else
         gpu_fail(g);
