@@ -511,7 +511,9 @@ def main():
         achieved = frame_bytes / (kern_ms_max / 1e3) / 1e9
         traffic, traffic_note = None, "no PMC profile for this config"
         tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                             f"traffic_{args.config}.json")
+                             # C4's per-GPU step is two launches of C2's shape (1 M x 1500 B
+                             # each): the per-launch figure is C2's
+                             f"traffic_{'c2' if args.config == 'c4' else args.config}.json")
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             if tj.get("lib_sha256") == lib_sha256():
@@ -524,6 +526,12 @@ def main():
             else:
                 traffic_note = (f"stale: {os.path.relpath(tpath)} was collected on another build "
                                 f"({tj.get('hbm_bytes_per_launch')} B per launch there)")
+            if traffic is not None and args.config == "c4":
+                # a C4 step (the unit of avg_launch_ms and of the algorithmic
+                # bytes here) is two launches of C2's shape: C2's per-launch
+                # traffic scaled by the frame bytes
+                traffic = round(traffic * frame_bytes / CONFIGS["c2"]["per_gpu"] / 1500)
+                traffic_note += "; C2's per-launch figure x the C4 step's frame bytes / C2's"
         line = {
             "metric": METRIC, "value": round(gbs, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
