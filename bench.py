@@ -143,27 +143,42 @@ def cpu_baseline(host_buf, desc, cfg, sample_n):
     buf = np.ascontiguousarray(host_buf[:end])
     nbytes = int(d["len"].astype(np.int64).sum())
     cores_all = cpu_share()
-    runs = {}
     kind = "reference" if oracle.ref_available() else "port"
-    for cores in sorted({1, cores_all}):
-        reps = 5
-        if kind == "reference":
-            best = oracle.ref_bench_rx(buf.copy(), d, 6, cfg["rss"], cores, reps)
-        else:
-            rss = oracle.rss_cfg(None, 8, 1) if cfg["rss"] else None
-            best = oracle.bench_rx(buf, d, 6, rss, cores, reps)
-        runs[cores] = dict(gbs=nbytes / best / 1e9, mpps=n / best / 1e6, seconds=best)
+
+    def measure(with_rss):
+        runs = {}
+        for cores in sorted({1, cores_all}):
+            reps = 5
+            if kind == "reference":
+                best = oracle.ref_bench_rx(buf.copy(), d, 6, with_rss, cores, reps)
+            else:
+                rss = oracle.rss_cfg(None, 8, 1) if with_rss else None
+                best = oracle.bench_rx(buf, d, 6, rss, cores, reps)
+            runs[cores] = dict(gbs=nbytes / best / 1e9, mpps=n / best / 1e6, seconds=best)
+        return runs
+
+    def per_core(runs):
+        return {str(c): {"GB/s": round(v["gbs"], 3), "Mpkt/s": round(v["mpps"], 3)}
+                for c, v in runs.items()}
+
+    runs = measure(cfg["rss"])
     best_cores = max(runs, key=lambda c: runs[c]["gbs"])
     r = runs[best_cores]
+    extra = {}
+    if cfg["rss"]:
+        # also without the per-packet Toeplitz hash (mTCP's own
+        # rx path does not hash per packet in software; the NIC does)
+        extra["without_rss"] = {"per_core_count": per_core(measure(False)),
+                                "note": "the same frames and code with GetRSSCPUCore not called"}
     return {
         "value": round(r["gbs"], 3), "unit": "GB/s", "cores": best_cores, "kind": kind,
         "mpkt_per_s": round(r["mpps"], 3),
         "sample": f"first {n} packets of the same batch ({nbytes} frame bytes), best of 5 "
                   f"after warm-up, one pinned thread per core on contiguous shards "
                   f"({'mtcp/src eth_in/ip_in/tcp_in/tcp_util compiled from /root/reference' if kind == 'reference' else 'oracle/mtcp_oracle.c restatement'}, gcc -O3)",
-        "per_core_count": {str(c): {"GB/s": round(v["gbs"], 3), "Mpkt/s": round(v["mpps"], 3)}
-                           for c, v in runs.items()},
+        "per_core_count": per_core(runs),
         "cpu_model": cpu_model(),
+        **extra,
     }
 
 
