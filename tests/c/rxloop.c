@@ -26,12 +26,17 @@
  *            so its own gpu_module context, GPU ctx and staging, and its own
  *            backend over a contiguous shard of the frames (share-nothing);
  *            the wall time runs from a common start barrier to the last
- *            thread's end
+ *            thread's end; thread t is pinned to the t-th CPU the process
+ *            may run on, as mtcp_core_affinitize (cpu.c) pins each mTCP
+ *            thread to its core (RXLOOP_CPUS=a,b,..: thread t on the t-th
+ *            CPU of that list; RXLOOP_PIN=0: unpinned)
  * Prints one JSON line with the counters and the wall time of the rx loop
  * (tools/io_path_bench.py turns that into the io_module path's rate).  Built with the test doubles in
  * tests/c/mtcp_double (two fields of mtcp_thread_context, io_module_func).
  */
+#define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -140,7 +145,7 @@ static void *slurp(const char *path, size_t *size)
 
 struct worker {
     pthread_t tid;
-    int cpu, timing, tx;
+    int cpu, pin_cpu, timing, tx;
     struct fake_psio fake;                 /* frames [first, first + fake.n) */
     uint32_t first;
     uint8_t *status;                       /* status + first */
@@ -173,12 +178,32 @@ static void tx_main(struct worker *w, struct mtcp_thread_context *ctx)
     }
 }
 
+/* The t-th CPU of the process's affinity mask (wraps), or -1. */
+static int nth_allowed_cpu(int t)
+{
+    cpu_set_t set;
+    int c, k = 0, count;
+    if (sched_getaffinity(0, sizeof(set), &set) != 0 || (count = CPU_COUNT(&set)) == 0)
+        return -1;
+    t %= count;
+    for (c = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &set) && k++ == t)
+            return c;
+    return -1;
+}
+
 static void *worker_main(void *arg)
 {
     struct worker *w = arg;
     struct mtcp_thread_context ctx = {w->cpu, NULL};
     const struct fake_psio *f = &w->fake;
 
+    if (w->pin_cpu >= 0) {                           /* before init_handle's allocations */
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(w->pin_cpu, &one);
+        pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+    }
     tl_fake = &w->fake;
     w->ioctl_ip = w->ioctl_tcp = -2;
     gpu_module_func.init_handle(&ctx);
@@ -281,6 +306,22 @@ int main(int argc, char **argv)
     status = calloc(n + 1, 1);
     if (tx) tx_buf = calloc(nb + 64, 1);
     ws = calloc((size_t)threads, sizeof(*ws));
+    const char *pin_env = getenv("RXLOOP_PIN");
+    const int pin = !(pin_env && strcmp(pin_env, "0") == 0);
+    int pin_cpu[64];
+    for (t = 0; t < threads; t++) pin_cpu[t] = pin ? nth_allowed_cpu(t) : -1;
+    const char *cpus_env = getenv("RXLOOP_CPUS");     /* "a,b,c": thread t -> t-th entry (wraps) */
+    if (pin && cpus_env && *cpus_env) {
+        int list[64], cnt = 0;
+        for (const char *c = cpus_env; *c && cnt < 64;) {
+            char *end;
+            long v = strtol(c, &end, 10);
+            if (end == c) break;
+            list[cnt++] = (int)v;
+            c = *end == ',' ? end + 1 : end;
+        }
+        for (t = 0; t < threads && cnt; t++) pin_cpu[t] = list[t % cnt];
+    }
 
     gpu_inner_module = &fake_module;
     gpu_module_func.load_module();
@@ -290,6 +331,7 @@ int main(int argc, char **argv)
         const uint32_t lo = (uint32_t)((uint64_t)n * t / threads);
         const uint32_t hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
         w->cpu = t;
+        w->pin_cpu = pin_cpu[t];
         w->timing = timing;
         w->tx = tx;
         w->fake.tx_buf = tx_buf;

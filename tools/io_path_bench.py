@@ -61,6 +61,40 @@ def reference(n, size, seed):
     return out
 
 
+def _cpulist(text):
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def host_topology():
+    """The process's CPUs, the GPU's NUMA node (sysfs of its PCI function)
+    and the CPUs of that node the process may use (all of its CPUs when the
+    node is unknown)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    node = -1
+    try:
+        pr = torch.cuda.get_device_properties(0)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read())
+    except (AttributeError, OSError, ValueError):
+        bdf = None
+    local = allowed
+    if node >= 0:
+        try:
+            with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+                cand = [c for c in _cpulist(f.read()) if c in set(allowed)]
+            local = cand or allowed
+        except OSError:
+            pass
+    return {"probe": "host_topology", "allowed_cpus": len(allowed), "allowed_first": allowed[:20],
+            "gpu_pci": bdf, "gpu_numa_node": node, "gpu_local_cpus": local[:32]}
+
+
 def run(n, size, seed, tmp, mode, threads=1, pipeline=True, tx=True):
     desc, host = frames(n, size, seed)
     bdesc = desc.copy()
@@ -124,6 +158,33 @@ def main():
         seeds = {64: 1, 1500: 2, "bimodal": 3}
         dump(n, size, seeds.get(size, 7), sys.argv[3])
         return
+    if "--threads-sweep" in sys.argv:
+        # thread scaling at 1500 B, timing mode: threads pinned to CPUs of
+        # the GPU's NUMA node, pinned to the first CPUs the process may use
+        # (as mtcp_core_affinitize pins thread i to core i), unpinned;
+        # interleaved twice
+        host = host_topology()
+        print(json.dumps(host), flush=True)
+        variants = ({"RXLOOP_CPUS": ",".join(map(str, host["gpu_local_cpus"]))},
+                    {}, {"RXLOOP_PIN": "0"})
+        with tempfile.TemporaryDirectory() as tmp:
+            for rep in range(2):
+                for knobs in variants:
+                    for k in ("RXLOOP_PIN", "RXLOOP_CPUS"):
+                        os.environ.pop(k, None)
+                    os.environ.update(knobs)
+                    for threads in (1, 2, 4, 8, 16):
+                        r = run(n, 1500, 2, tmp, "timing", threads, True)
+                        print(json.dumps({"probe": "io_thread_sweep", "rep": rep, "knobs": knobs,
+                                          "threads": threads, "frames": n,
+                                          "mpkt_per_s": r["mpkt_per_s"], "GBs": r["GBs"]}),
+                              flush=True)
+            for k in ("RXLOOP_PIN", "RXLOOP_CPUS"):
+                os.environ.pop(k, None)
+            ref = reference(n, 1500, 2)
+            if ref:
+                print(json.dumps(ref), flush=True)
+        return
     if "--quick" in sys.argv:
         # A/B of the staging knobs (rxq.hip): 1 thread, 1500 B, timing and verify
         with tempfile.TemporaryDirectory() as tmp:
@@ -146,6 +207,12 @@ def main():
             if ref:
                 print(json.dumps(ref), flush=True)
         return
+    # mTCP threads on the GPU's NUMA node (tools/io_path_bench.py
+    # --threads-sweep: pinned to the other socket's cores, 2-4 threads ran
+    # 24-29 Mpkt/s against 33-35)
+    host = host_topology()
+    print(json.dumps(host), flush=True)
+    os.environ.setdefault("RXLOOP_CPUS", ",".join(map(str, host["gpu_local_cpus"])))
     with tempfile.TemporaryDirectory() as tmp:
         for size, seed in ((1500, 2), (64, 1), ("bimodal", 3)):
             for mode, pipeline in (("timing", True), ("payload", True), ("timing", False), ("verify", True)):
