@@ -314,6 +314,99 @@ __device__ __forceinline__ Pkt parse_head(PD pd, IPSUM ipsum, SW sw, SWB swb, ui
     return k;
 }
 
+// parse_head_sel: the per-lane form (rx_kernel and the grouped kernels,
+// through parse_finish), with the same results as parse_head above, for
+// callers whose pd(i) is readable for every i <= 22 (a staged copy, past the
+// frame's end too) and whose ipsum(ihl) takes any ihl.  Single exit: every candidate field is computed from the header dwords and kept
+// only where the reference's chain reaches it (the step's length check
+// passed); the verdict is a select chain in the reference's check order.  The
+// early-return form costs a divergent branch, an exec-mask save and a
+// re-zeroing of every record field per check when lanes parse different
+// packets (quad kernel phase 2: 1071 -> 907 instructions, 64 K x 64 B
+// 5.1 -> 4.8 us).  A wave parsing ONE packet (rx_wave_kernel) keeps the
+// early-return form: its branches are scalar and nearly free, while the
+// selects cost scalar-unit issue slots, its bound (4 096 x 1500 B 3.9 ->
+// 4.4 us with this form).
+template <int MODE, class PD, class IPSUM, class SW, class SWB>
+__device__ __forceinline__ Pkt parse_head_sel(PD pd, IPSUM ipsum, SW sw, SWB swb, uint32_t L,
+                                          bool desc_ok) {
+    constexpr bool tx = is_tx(MODE);
+    const uint32_t d0 = pd(3), h4 = pd(4), h5 = pd(5), h6 = pd(6);     // bytes 12..27
+    const uint32_t eth = bswap16(d0 & 0xFFFFu);                           // eth_in.c:13
+    const uint32_t ipl = bswap16(h4 & 0xFFFFu);                           // ip_in.c:21
+    const uint32_t ihl = (d0 >> 16) & 0xFu, ver = (d0 >> 20) & 0xFu;
+    const uint32_t proto = h5 >> 24;                                      // ip_in.c:52
+    const uint32_t T = 14 + 4 * ihl;
+    // how far the chain gets: the frame holds the Ethernet header, it is
+    // IPv4, tot_len is readable, passes ip_len >= 20 (rx), and the IP header
+    // lies inside the frame (ip_fast_csum reads 4*ihl bytes, at least 4)
+    const bool ok14 = desc_ok && L >= 14;
+    const bool isip = ok14 && eth == 0x0800u;
+    const bool ok18 = isip && L >= 18;
+    const bool shrt = !tx && ipl < 20;                                    // ip_in.c:25-26
+    const bool okhdr = ok18 && !shrt && L >= 14 + 4 * (ihl > 1 ? ihl : 1);
+    // ip_fast_csum: ihl <= 4 returns dword 0 as is (ps.h:72-73)
+    const uint32_t s_ip = ipsum(ihl);
+    const uint32_t ip_csum = ihl <= 4 ? (d0 >> 16) : fold_csum(s_ip);
+    const bool ip_good = okhdr && ip_csum == 0 && ver == 4;              // ip_in.c:35-50
+    // tcp_in.c:1142-1149: tcph = iph + 4*ihl (T = 4 tw + 2)
+    const uint32_t tw = (T - 2) >> 2;
+    const uint32_t e3 = pd(tw + 3), e4 = pd(tw + 4);
+    const uint32_t doff = (e3 >> 20) & 0xFu;
+    const bool tcp_entry = tx ? okhdr && ver == 4 && ihl >= 5 && proto == 6 && L >= T + 20
+                              : ip_good && proto == 6 && L >= T + 16;
+    const uint32_t hlen = (ihl + doff) << 2;
+    const bool in_frame = 14 + ipl <= L;                                  // the datagram is readable
+    const bool len_bad = !tx && tcp_entry && ipl < hlen;                  // tcp_in.c:1155-1156
+    // ICMPChecksum(icmph, ip_len - 4*ihl) (icmp.c:18-42), the echo-request
+    // check of icmp.c:94, when the datagram lies inside the frame; a negative
+    // length skips the loop: ~0
+    const bool icmp_in = !tx && ip_good && proto == 1 && in_frame;
+    const bool icmp = icmp_in && ipl >= 4 * ihl;
+    const bool tcp_sum = tx ? tcp_entry && doff >= 5 && ipl >= hlen && in_frame
+                            : tcp_entry && !len_bad && in_frame;          // tcp_in.c:1166
+
+    uint32_t v = MTCP_GPU_V_TRUNCATED;                  // no check failed, the TCP sum pending
+    if (!tx) {
+        v = len_bad ? MTCP_GPU_V_TCP_LEN_BAD : v;
+        v = ip_good && proto != 6 ? MTCP_GPU_V_IP_PROTO_OTHER : v;        // ip_in.c:57-59
+        v = ip_good && proto == 1 ? MTCP_GPU_V_ICMP : v;
+        v = okhdr && ip_csum == 0 && ver != 4 ? MTCP_GPU_V_IP_VERSION : v; // ip_in.c:47-50
+        v = okhdr && ip_csum != 0 ? MTCP_GPU_V_IP_CSUM_BAD : v;           // ip_in.c:35-36
+        v = ok18 && shrt ? MTCP_GPU_V_IP_SHORT : v;
+    } else {
+        v = okhdr ? MTCP_GPU_V_ETH_OTHER : v;
+    }
+    v = ok14 && !isip ? (eth == 0x0806u ? MTCP_GPU_V_ARP : MTCP_GPU_V_ETH_OTHER) : v;
+    v = desc_ok ? v : MTCP_GPU_V_BAD_DESC;
+
+    Pkt k;
+    k.verdict = v;
+    k.eth_type = ok14 ? eth : 0u;
+    k.ip_len = ok18 ? ipl : 0u;
+    k.ihl_doff = ok18 ? ihl | (tcp_entry ? doff << 4 : 0u) : 0u;
+    k.s_ip = okhdr && ihl >= 5 ? s_ip : 0u;
+    k.ip_check = okhdr ? h6 & 0xFFFFu : 0u;
+    k.ip_csum = okhdr ? ip_csum : 0u;
+    k.T = okhdr ? T : 0u;
+    k.tcp_entry = tcp_entry;
+    k.saddr = tcp_entry ? sw(6) : 0u;                                     // bytes 26..29
+    k.daddr = tcp_entry ? sw(7) : 0u;                                     // bytes 30..33
+    k.ports = tcp_entry ? sw(tw) : 0u;                                    // sport | dport << 16
+    k.seq = tcp_entry ? swb(tw + 1) : 0u;
+    k.ack = tcp_entry ? swb(tw + 2) : 0u;
+    k.window = tcp_entry ? bswap16(e4 & 0xFFFFu) : 0u;
+    k.flags = tcp_entry ? e3 >> 24 : 0u;
+    k.tcheck = tcp_entry ? e4 >> 16 : 0u;
+    k.icmp = icmp;
+    k.need_sum = tcp_sum || icmp;
+    k.seg_len = k.need_sum ? ipl - 4 * ihl : 0u;
+    k.payload_len = icmp ? ipl - 4 * ihl                                  // icmp.c:94's length
+                  : !tx && tcp_entry && !len_bad ? ipl - hlen : 0u;       // tcp_in.c:1144
+    k.tcp_csum = icmp_in && !icmp ? 0xFFFFu : 0u;
+    return k;
+}
+
 // The checksum from the exact word sum of the segment [T, 14 + ip_len):
 // TCPCalcChecksum's pseudo header and two-step fold (tcp_util.c:157-190),
 // or ICMPChecksum's fold (icmp.c:36-38); the rx verdict (tcp_in.c:1167-1173).
@@ -364,7 +457,7 @@ __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, u
     };
     auto sw = [&](uint32_t i) -> uint32_t { return __builtin_amdgcn_alignbit(pd(i + 1), pd(i), 16); };
     auto swb = [&](uint32_t i) -> uint32_t { return bswap32(sw(i)); };
-    Pkt k = parse_head<MODE>(pd, ipsum, sw, swb, L, desc_ok);
+    Pkt k = parse_head_sel<MODE>(pd, ipsum, sw, swb, L, desc_ok);
     if (k.need_sum) {
         // The chunk sum covers [p16, p16 + 16*nch).  Remove the bytes before
         // the frame, the header bytes [0, T), and everything at or past
