@@ -436,9 +436,7 @@ __device__ __forceinline__ void finish_seg(Pkt &k, uint32_t seg) {
 // 8 * (sh & 3) bits, and each 16-bit word of the packet is still a whole
 // half of one aligned dword, which keeps the sum exact.  The segment sum is
 // the chunk sum minus the bytes outside [T, 14 + ip_len).
-// BULK: the header dwords that the subtraction needs are read from LDS in one
-// batch instead of one conditional read per dword.
-template <int MODE, int S, bool BULK = false>
+template <int MODE, int S>
 __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, uint64_t p,
                                             uint32_t L, uint32_t nch, bool desc_ok) {
     const uint32_t sh = (uint32_t)(p & 15);
@@ -462,28 +460,18 @@ __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, u
         // The chunk sum covers [p16, p16 + 16*nch).  Remove the bytes before
         // the frame, the header bytes [0, T), and everything at or past
         // E = 14 + ip_len.
-        uint32_t s_out = 0;
-        // (a) bytes [p16, p + T): whole raw dwords, then the low half of the
-        //     next one when sh + T ends mid-dword (T = 14 + 4*ihl is even)
-        const uint32_t nb = sh + k.T;
-        const int whole = (int)(nb >> 2);              // <= (14 + 74) / 4 = 22
-        if constexpr (BULK) {
-            uint32_t rw[23], low = 0;
+        // (a) bytes [p16, p + T): the bytes of chunk 0 before the frame (raw
+        //     dwords 0..a-1, and the low half of dword a when sh & 2), the
+        //     Ethernet header (frame words 0..6: packet dwords 0..2 and the
+        //     low half of dword 3) and the IP header [14, T), whose exact
+        //     word sum s_ip the IP checksum already took (a segment is summed
+        //     only past an IP header that passed, so ihl >= 5)
+        uint32_t s_out = k.s_ip + (pd(3) & 0xFFFFu);
+        s_out = halves(pd(2), halves(pd(1), halves(pd(0), s_out)));
 #pragma unroll
-            for (int i = 0; i < 23; ++i) rw[i] = raw[i * S];
-#pragma unroll
-            for (int i = 0; i < 23; ++i) {
-                s_out = halves(i < whole ? rw[i] : 0u, s_out);
-                if (i == whole) low = rw[i] & 0xFFFFu;
-            }
-            if (nb & 2) s_out += low;
-        } else {
-#pragma unroll
-            for (int i = 0; i < 28; ++i) {
-                if (i < whole) s_out = halves(raw[i * S], s_out);
-            }
-            if (nb & 2) s_out += raw[whole * S] & 0xFFFFu;
-        }
+        for (uint32_t i = 0; i < 3; ++i)
+            if (i < a) s_out = halves(raw[i * S], s_out);
+        if (sh & 2) s_out += raw[a * S] & 0xFFFFu;
         // (b) bytes [p + E, p16 + 16*nch)
         const uint64_t p16 = p & ~15ull;
         const uint64_t e_abs = p + 14 + k.ip_len;

@@ -420,7 +420,7 @@ __global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
         kp.out[kk].saddr = sum;
         return;
     }
-    const Pkt pk = parse_finish<MODE, S, true>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);
+    const Pkt pk = parse_finish<MODE, S>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);
     if constexpr (is_tx(MODE)) {
         const uint32_t checks = fold_csum(pk.s_ip - pk.ip_check) | (pk.tcp_csum << 16);
         if (kp.tx_report) {
