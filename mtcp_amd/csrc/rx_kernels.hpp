@@ -445,11 +445,14 @@ __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, u
         return __builtin_amdgcn_alignbit(raw[(a + i + 1) * S], raw[(a + i) * S], fb);
     };
     auto ipsum = [&](uint32_t ihl) -> uint32_t {  // words [14, 14 + 4*ihl): dwords 3..3+ihl
+        // every dword read, the ones past the header masked: no per-dword
+        // branch (the staged rows reach pd(18))
         uint32_t s_ip = pd(3) >> 16, lo_last = 0;
 #pragma unroll
         for (int j = 1; j < 16; ++j) {
-            if (j < (int)ihl) s_ip = halves(pd(3 + j), s_ip);
-            if (j == (int)ihl) lo_last = pd(3 + j) & 0xFFFFu;
+            const uint32_t w = pd(3 + j);
+            s_ip = halves(j < (int)ihl ? w : 0u, s_ip);
+            lo_last = j == (int)ihl ? w & 0xFFFFu : lo_last;
         }
         return s_ip + lo_last;
     };
