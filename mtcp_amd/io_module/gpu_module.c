@@ -80,6 +80,7 @@
 #define GPU_BURST      64                 /* PS_CHUNK_SIZE / MAX_PKT_BURST   */
 #define GPU_RXQ_PKTS   (GPU_AGG_BURSTS * GPU_BURST)
 #define GPU_FRAME_MAX  2048ull            /* MAX_PACKET_SIZE (ps.h:173)      */
+#define GPU_FRAME_JUMBO 9216ull           /* the largest frame a burst is expected to bring */
 #define GPU_TX_MAX     4096               /* frames recorded between two send_pkts */
 
 /* the backend being wrapped (e.g. &ps_module_func or &dpdk_module_func) */
@@ -329,19 +330,33 @@ static uint32_t gather(struct mtcp_thread_context *ctx, struct gpu_ifq *f, int i
     struct gpu_private_context *g = ctx->io_private_context;
     mtcp_gpu_rxq *q = f->rxq[a];
     uint32_t total = 0;
+    uint64_t bytes = 0;                              /* staging used (64 B slots) */
     int b, i;
 
     mtcp_gpu_rxq_reset(q);
     for (b = 0; b < GPU_AGG_BURSTS; b++) {
-        int32_t n = INNER_CALL(ctx, gpu_inner_module->recv_pkts(ctx, ifidx));
+        int32_t n;
+        /* a burst is only pulled when the staging holds it even if every
+         * frame is jumbo: a received burst cannot be left half staged (the
+         * backend recycles its buffers on the next receive) */
+        if (bytes + GPU_BURST * GPU_FRAME_JUMBO > GPU_RXQ_PKTS * GPU_FRAME_MAX)
+            break;
+        n = INNER_CALL(ctx, gpu_inner_module->recv_pkts(ctx, ifidx));
         if (n <= 0)
             break;
         for (i = 0; i < n && total < GPU_RXQ_PKTS; i++) {
             uint16_t len = 0;
             uint8_t *p = INNER_CALL(ctx, gpu_inner_module->get_rptr(ctx, ifidx, i, &len));
             f->dropped[a][total] = (p == NULL);
-            if (mtcp_gpu_rxq_push(q, p, p ? len : 0) != MTCP_GPU_OK)
-                break;
+            if (mtcp_gpu_rxq_push(q, p, p ? len : 0) == MTCP_GPU_OK) {
+                bytes += p ? ((uint64_t)len + 63) & ~63ull : 0;
+            } else {
+                /* larger than the room left (a frame above GPU_FRAME_JUMBO):
+                 * served as NULL, counted in rx_errors (core.c:772-775) */
+                f->dropped[a][total] = 1;
+                if (mtcp_gpu_rxq_push(q, NULL, 0) != MTCP_GPU_OK)
+                    break;                           /* cannot happen: total < GPU_RXQ_PKTS */
+            }
             total++;
         }
         if (n < GPU_BURST || total + GPU_BURST > GPU_RXQ_PKTS)

@@ -154,3 +154,39 @@ def test_gpu_module_tx_off_leaves_checksums_to_mtcp(tmp_path, golden):
     stats, sent = run_rxloop(tmp_path, mode="tx")
     assert stats["ioctl_tx"] == -1 and stats["sw_filled"] == golden.manifest["tx_filled"]
     assert np.array_equal(sent, tx_expect(golden))
+
+
+@pytest.mark.gpu
+def test_gpu_module_jumbo_bursts_never_lose_frames(tmp_path):
+    """Frames larger than the staging's 2 KiB slots (jumbo MTU): an aggregate
+    stops pulling bursts before a burst of jumbo frames could overflow the
+    staging (a received burst cannot be left half staged: the backend
+    recycles its buffers on the next receive), so every frame is served —
+    byte-identical — or dropped for its checksum, as with MTU frames."""
+    import torch
+    import oracle
+    from mtcp_amd import gpu, pktgen
+    n, seed = 8192, 5
+    desc, nbytes = pktgen.layout(n, 9000, 6, seed)
+    dev = torch.device("cuda", 0)
+    d_buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+    gpu.pktgen_dev(d_buf, d_desc, n, 6, seed)
+    host = d_buf.cpu().numpy()
+    bdesc = desc.copy()
+    bdesc["offset"] = desc["offset"] << 6                # rxloop takes byte offsets
+    chunk, dpath, status_path = tmp_path / "chunk.bin", tmp_path / "desc.bin", tmp_path / "status.bin"
+    host.tofile(chunk)
+    bdesc.tofile(dpath)
+    p = subprocess.run([build_rxloop(), str(chunk), str(dpath), str(status_path), "verify", "1"],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MTCP_GPU_PIPELINE="1", MTCP_GPU_TX="0"))
+    assert p.returncode == 0, p.stderr
+    stats = json.loads(p.stdout.strip().splitlines()[-1])
+    status = np.fromfile(status_path, dtype=np.uint8)
+    v = oracle.rx_chunk(host, desc, 6)["verdict"]
+    drop = (v == V_IP_CSUM_BAD) | (v == V_TCP_CSUM_BAD) | (v == V_TRUNCATED)
+    assert stats["seen"] == stats["frames"] == n
+    assert np.array_equal(status == 0, drop) and drop.sum() > 0
+    assert (status[~drop] == 1).all() and stats["changed"] == 0
+    assert stats["ioctl_rx_ip"] == 0 and stats["ioctl_rx_tcp"] == 0
