@@ -206,11 +206,14 @@ constexpr uint32_t kHeldPasses = 8;
 // quad) on every packet.  The choice by batch size and average slot, from
 // tools/wave_probe.hip and tools/small_batch_probe.py (same frames, same
 // process):
-//   n <= 4 096                       one wavefront per packet
-//   slot > 4 KiB, n <= 64 K          one wavefront per packet (a jumbo frame in one trip)
-//   slot < 256 B, n <= 64 K          a quad per packet, 256 packets per workgroup
-//   n <= 32 K                        a row per packet, 64 packets per workgroup
-//   otherwise                        rx_kernel (64 packets per wave)
+//   slot < 256 B:   n <= 2 048  wave;  n <= 128 K a quad per packet (256 per workgroup)
+//   slot > 4 KiB:   n <= 64 K   wave (a jumbo frame in one trip)
+//   otherwise:      n <= 8 192  wave;  n <= 32 K  a row per packet (64 per workgroup)
+//   larger batches: rx_kernel (64 packets per wave)
+// (since the select-form per-lane phase 2: 4 096 x 64 B quad 3.55 vs wave
+// 3.86 us, 2 048 x 64 B 3.53 vs 3.21; 8 192 x 1500 B wave 6.05 vs row 7.32,
+// 16 K 9.31 vs 7.35: profiles/r2/wave_probe_dispatch.jsonl; 128 K x 64 B quad 5.37
+// vs rx_kernel 6.05 us through the Python ABI: profiles/r2/small_batch_sched.jsonl)
 // Pointer bursts carry no size the host can see: they count as mid-size.
 // MTCP_GPU_SCHED=wave|row|quad|big at context open forces one kernel for
 // every batch (A/B runs, and the parity tests of each); the tx fill of
@@ -230,10 +233,9 @@ int sched_from_env() {
 int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_only) {
     int s = ctx->sched;
     if (s == kSchedAuto) {
-        if (n <= 4096) s = kSchedWave;
+        if (slot < 256) s = n <= 2048 ? kSchedWave : n <= (1u << 17) ? kSchedQuad : kSchedBig;
         else if (slot > 4096) s = n <= (1u << 16) ? kSchedWave : kSchedBig;
-        else if (slot < 256) s = n <= (1u << 16) ? kSchedQuad : kSchedBig;
-        else s = n <= (1u << 15) ? kSchedRow : kSchedBig;
+        else s = n <= 8192 ? kSchedWave : n <= (1u << 15) ? kSchedRow : kSchedBig;
     }
     if (s == kSchedBig && small_only) s = kSchedRow;
     return s;
