@@ -36,53 +36,6 @@
 
 namespace mg {
 
-// parse_head_wave: parse_head for a wave parsing one packet (rx_wave_kernel),
-// with the common rx frame — Ethernet IPv4 (version 4, ihl 5) carrying TCP,
-// tot_len >= 20, its headers inside the frame, the IP checksum good — taken
-// on one straight path with one exit; every other frame goes through
-// parse_head's chain.  Same results (the checks below are the chain's own
-// for ihl = 5: ip_in.c:25-60, tcp_in.c:1142-1156).
-template <int MODE, class PD, class IPSUM, class SW, class SWB>
-__device__ __forceinline__ Pkt parse_head_wave(PD pd, IPSUM ipsum, SW sw, SWB swb, uint32_t L,
-                                               bool desc_ok) {
-    if constexpr (!is_tx(MODE)) {
-        const uint32_t d0 = pd(3), h4 = pd(4), h5 = pd(5);              // bytes 12..23
-        const uint32_t ipl = bswap16(h4 & 0xFFFFu);
-        // bytes 12..14 = 08 00 45: ethertype IPv4, version 4, ihl 5; protocol 6;
-        // L >= T + 16 with T = 34
-        if (desc_ok && L >= 50 && (d0 & 0xFFFFFFu) == 0x450008u && (h5 >> 24) == 6u && ipl >= 20u) {
-            const uint32_t s_ip = ipsum(5);
-            if (fold_csum(s_ip) == 0) {
-                const uint32_t e3 = pd(11), e4 = pd(12);                  // tcph bytes 12..19
-                const uint32_t doff = (e3 >> 20) & 0xFu, hlen = (5 + doff) << 2;
-                const bool len_bad = ipl < hlen;
-                Pkt k;
-                k.verdict = len_bad ? MTCP_GPU_V_TCP_LEN_BAD : MTCP_GPU_V_TRUNCATED;
-                k.eth_type = 0x0800u;
-                k.ip_len = ipl;
-                k.ihl_doff = 5u | (doff << 4);
-                k.s_ip = s_ip;
-                k.ip_check = pd(6) & 0xFFFFu;
-                k.T = 34;
-                k.tcp_entry = true;
-                k.saddr = sw(6);
-                k.daddr = sw(7);
-                k.ports = sw(8);
-                k.seq = swb(9);
-                k.ack = swb(10);
-                k.window = bswap16(e4 & 0xFFFFu);
-                k.flags = e3 >> 24;
-                k.tcheck = e4 >> 16;
-                k.payload_len = len_bad ? 0u : ipl - hlen;
-                k.need_sum = !len_bad && 14 + ipl <= L;
-                k.seg_len = k.need_sum ? ipl - 20 : 0u;
-                return k;
-            }
-        }
-    }
-    return parse_head<MODE>(pd, ipsum, sw, swb, L, desc_ok);
-}
-
 constexpr int kWaveLoads = 10;  // 16 B loads per lane per trip: 10 KiB of frame (a 9000 B frame in one)
 
 // XOR over the 64 lanes (DPP row_shr steps, then the four row results).
@@ -467,7 +420,7 @@ __global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
         kp.out[kk].saddr = sum;
         return;
     }
-    const Pkt pk = parse_finish<MODE, S>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);
+    const Pkt pk = parse_finish<MODE, S, true>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);
     if constexpr (is_tx(MODE)) {
         const uint32_t checks = fold_csum(pk.s_ip - pk.ip_check) | (pk.tcp_csum << 16);
         if (kp.tx_report) {
