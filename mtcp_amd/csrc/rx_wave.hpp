@@ -16,8 +16,9 @@
 //            reduction and four readlanes give the frame's chunk sum in an
 //            SGPR.  Chunks 0..6 (the headers) and the last chunk go to the
 //            wave's 128 B of LDS.
-//   phase 2  parse_head / finish_seg (rx_kernels.hpp, the code rx_kernel
-//            runs per lane) on the whole wave with wave-uniform operands: one
+//   phase 2  parse_head_wave / finish_seg (rx_kernels.hpp: the common frame
+//            on one straight path, parse_head's chain for every other one)
+//            on the whole wave with wave-uniform operands: one
 //            instruction stream per packet, mostly scalar.  The CU's one
 //            scalar unit serves its 16 waves of a 4 096-packet batch, so the
 //            SALU count per packet sets phase 2's time (PMC, 4 096 x 1500 B:
