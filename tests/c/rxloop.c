@@ -374,6 +374,11 @@ int main(int argc, char **argv)
         printf("{\"frames\": %u, \"sent\": %u, \"send_calls\": %d, \"ioctl_tx\": %d, "
                "\"sw_filled\": %d, \"seconds\": %.6f, \"frame_bytes\": %llu, \"threads\": %d}\n",
                n, sent, sends, ws[0].ioctl_tx, sw, secs, (unsigned long long)frame_bytes, threads);
+        free(tx_buf);
+        free(ws);
+        free(status);
+        free((void *)buf);
+        free((void *)desc);
         return 0;
     }
     if (!out || fwrite(status, 1, n, out) != n) { perror(argv[3]); return 1; }
@@ -387,5 +392,9 @@ int main(int argc, char **argv)
            (unsigned long long)rx_errors, (unsigned long long)changed, ws[0].ioctl_ip,
            ws[0].ioctl_tcp, secs, (unsigned long long)frame_bytes, timing,
            (unsigned long long)hdr_sum, threads);
+    free(ws);
+    free(status);
+    free((void *)buf);
+    free((void *)desc);
     return 0;
 }
