@@ -664,6 +664,10 @@ struct Trip {
 // {start, end} of s_memrealtime (100 MHz), HW_REG_XCC_ID and HW_REG_HW_ID to
 // kp.stamps[4 * wave ...].
 // WPB: waves per workgroup (the grid then holds 8 / WPB workgroups per CU).
+// XSKIP (timing probe only, tools/rx_variants "abl_xskip*": its records are
+// wrong): in the last pass, the waves on odd XCDs (XSKIP > 0) or on even
+// ones (XSKIP < 0) leave their last |XSKIP| frames unread — how much a
+// launch would gain if work moved between the XCD groups.
 // PRIO: the second workgroup on each CU (blockIdx >= gridDim / 2; the
 // dispatcher fills every CU once before the second round) runs at
 // s_setprio(PRIO & 3): the older wave of a SIMD otherwise wins its issue
@@ -671,7 +675,7 @@ struct Trip {
 // passes.
 template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
           bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0,
-          int WPB = kWavesPerBlock>
+          int WPB = kWavesPerBlock, int XSKIP = 0>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
     uint64_t t_start = 0;
     if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
@@ -697,6 +701,11 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))
         return B == kWave ? wave * kWave + l : (l / B) * (nwaves * B) + wave * B + (l % B);
     };
     const uint32_t lane_off = map(lane);
+    bool xskip_wave = false;
+    if constexpr (XSKIP != 0) {
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 1u;  // HW_REG_XCC_ID[0]
+        xskip_wave = XSKIP > 0 ? xcc == 1u : xcc == 0u;
+    }
     const uint64_t safe = (uint64_t)(uintptr_t)(MODE == kRxPtrs ? (const void *)kp.out
                                                                : (const void *)kp.buf);
     // the packet of this lane in pass g0, and whether the batch has it
@@ -727,6 +736,10 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))
         bool live;
         (void)lane_pkt(g0, live);
         f.live = live;
+        if constexpr (XSKIP != 0) {
+            if (xskip_wave && g0 + pass_pkts >= kp.n && lane >= (uint32_t)(kWave - (XSKIP > 0 ? XSKIP : -XSKIP)))
+                f.live = false;
+        }
         f.p = safe;
         f.L = 0;
         f.ok = false;

@@ -620,6 +620,12 @@ int main(int argc, char **argv) {
         vs.push_back({"unrolled_wpb2_cu4", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 2>, 4, 2});
         vs.push_back({"unrolled_lalign_rev_wpb8_cu1", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, false, 0, 8>, 1, 8});
         vs.push_back({"unrolled_prio1half_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 5>, 2});
+        // XCD balance probe (records wrong: compared with nothing): odd / even
+        // XCD waves leave their last 8 / 16 / 24 frames of the last pass unread
+        vs.push_back({"abl_xskip_odd8_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 5, 4, 8>, 2});
+        vs.push_back({"abl_xskip_odd16_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 5, 4, 16>, 2});
+        vs.push_back({"abl_xskip_odd24_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 5, 4, 24>, 2});
+        vs.push_back({"abl_xskip_even16_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 5, 4, -16>, 2});
         vs.push_back({"unrolled_prio2half_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 6>, 2});
         vs.push_back({"unrolled_lalign_rev_prio1half_cu2", rx_kernel<kRxChunk, false, 3, true, 0, 8, 8, true, 6, true, false, 5>, 2});
         vs.push_back({"unrolled_prio1_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 1>, 2});
