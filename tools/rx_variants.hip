@@ -594,6 +594,9 @@ int main(int argc, char **argv) {
         vs.push_back({"rss_sorted5_cu2", rx_kernel<kRxChunk, true, 5>, 2});
         vs.push_back({"rss_sorted6_cu3", rx_kernel<kRxChunk, true, 6>, 3});
         vs.push_back({"rss_sorted6_defer0_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 0>, 2});
+        vs.push_back({"rss_sorted6_defer1_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 1>, 2});
+        vs.push_back({"rss_sorted6_defer2_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 2>, 2});
+        vs.push_back({"rss_sorted6_defer4_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 4>, 2});
         vs.push_back({"abl1_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 1>, 2});
         vs.push_back({"abl2_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 2>, 2});
         vs.push_back({"abl1_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0>, 2});
