@@ -103,6 +103,21 @@ def test_small_batches_every_schedule(gpu, monkeypatch, n, size, rss):
     assert (want["verdict"] == 0).mean() > 0.99
 
 
+@pytest.mark.parametrize("n,size", [(2048, 64), (2049, 64), (1 << 17, 64), (8192, 1500), (8193, 1500)])
+def test_dispatch_boundaries(gpu, monkeypatch, n, size):
+    """The automatic kernel choice (mtcp_gpu.hip pick_sched) on both sides of
+    each boundary it draws — small frames: wave up to 2 048, quad up to
+    128 K; MTU frames: wave up to 8 192, row above — equal to the oracle."""
+    monkeypatch.delenv("MTCP_GPU_SCHED", raising=False)
+    seed = 67
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    want = oracle.rx_chunk(buf, desc, 6)
+    with gpu.Context(0) as ctx:
+        assert_same(run_rx_dev(ctx, buf, desc, 6), want, f"auto {size} x {n}")
+
+
 def test_short_trip_kernel_with_jumbo_frames(gpu, monkeypatch):
     """A batch whose average slot is at most 2 KiB takes the wave kernel's
     2-load trips (mtcp_gpu.hip kWaveShortUpToSlot): its jumbo frames then
