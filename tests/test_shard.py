@@ -53,13 +53,13 @@ def _worker(rank, world, port, size, n, seed, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("size", [1500, "bimodal"])
-def test_two_rank_shards_equal_full_batch(size):
+@pytest.mark.parametrize("size,world", [(1500, 2), ("bimodal", 2), ("bimodal", 4)])
+def test_two_rank_shards_equal_full_batch(size, world):
     n, seed = 3000, 11
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() % 1000)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, size, n, seed, q)) for r in range(2)]
+    port = 29500 + (os.getpid() % 1000) + 7 * world
+    procs = [ctx.Process(target=_worker, args=(r, world, port, size, n, seed, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
