@@ -15,10 +15,12 @@ nothing), and --dump-records DIR writes each rank's result records after the
 timed steps (tests/test_gpu_shard.py compares them with one launch over the
 whole batch).
 
-Multi-GPU: one process per GPU (torch.distributed.run), weak scaling — each
+Multi-GPU: one process per GPU, weak scaling — each
 rank processes its own contiguous shard of one global batch (batch split, no
 collective on the data path; gloo carries only the barrier and the max of the
-per-rank times).  Rank 0 prints ONE JSON line.
+per-rank times).  Rank 0 prints ONE JSON line.  Under torch.distributed.run
+(WORLD_SIZE set) each process is one rank; `python bench.py --gpus N` with no
+launcher starts its N ranks itself (self_launch) and forwards that line.
 
 The CPU baseline (rank 0, N=1 only) times the reference's own rx code
 (oracle/_ref/libref_rx.so, compiled from /root/reference) or, where that
@@ -30,6 +32,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -404,11 +407,66 @@ def run_row(args):
     print(json.dumps(line), flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(argv, n, port):
+    """The rank launcher bench.py starts for `--gpus N` without one:
+    torch.distributed.run, one process per GPU on this node, rendezvous on
+    127.0.0.1 (the container's hostname may not resolve)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__), *argv]
+
+
+def self_launch(args, argv) -> int:
+    """`python bench.py --gpus N` (N > 1) with no WORLD_SIZE in the
+    environment: start the N rank processes here, as mTCP starts its own
+    per-core workers (mtcp_create_context -> pthread_create /
+    rte_eal_remote_launch, mtcp/src/core.c:1195-1213).  Nothing in this
+    parent touches the GPU (no torch.cuda call: the ranks are fresh child
+    processes, never an exec of a process that initialised HIP).  The ranks'
+    JSON line (rank 0 prints one) is forwarded to stdout, everything else to
+    stderr; the exit status is the launcher's (non-zero if any rank failed)."""
+    import subprocess
+    if "MTCP_BENCH_DEVICE" not in os.environ:
+        # device_count() does not initialise HIP on this image; a clear error
+        # beats N ranks dying in set_device
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible "
+                  f"(MTCP_BENCH_DEVICE=d puts every rank on device d)", file=sys.stderr)
+            return 2
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.Popen(launch_cmd(argv, args.gpus, _free_port()), env=env,
+                         stdout=subprocess.PIPE, text=True, bufsize=1)
+    lines = 0
+    for ln in p.stdout:
+        if ln.startswith("{"):
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+            lines += 1
+        else:
+            sys.stderr.write(ln)
+    rc = p.wait()
+    if rc == 0 and lines != 1:
+        print(f"bench.py: the ranks printed {lines} JSON lines, expected 1", file=sys.stderr)
+        return 3
+    return rc
+
+
 def main():
     args = parse()
     if args.config in ROWS:
         return run_row(args)
     cfg = CONFIGS[args.config]
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(self_launch(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

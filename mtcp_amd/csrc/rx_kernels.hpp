@@ -248,7 +248,7 @@ __device__ __forceinline__ Pkt parse_head(PD pd, IPSUM ipsum, SW sw, SWB swb, ui
         k.verdict = MTCP_GPU_V_IP_SHORT;                                   // ip_in.c:25-26
         return k;
     }
-    if (L < 14 + 4 * (ihl > 1 ? ihl : 1)) return k;
+    if (L < 14 + 4 * (ihl > 4 ? ihl : 1)) return k;   // ps.h:68-70: ihl <= 4 reads one dword
     // ip_fast_csum: ihl <= 4 returns dword 0 as is (ps.h:72-73)
     if (ihl >= 5) k.s_ip = ipsum(ihl);
     k.ip_check = h[6] & 0xFFFFu;
@@ -400,12 +400,13 @@ __device__ __forceinline__ Pkt parse_head_sel(PD pd, IPSUM ipsum, SW sw, SWB swb
     const uint32_t T = 14 + 4 * ihl;
     // how far the chain gets: the frame holds the Ethernet header, it is
     // IPv4, tot_len is readable, passes ip_len >= 20 (rx), and the IP header
-    // lies inside the frame (ip_fast_csum reads 4*ihl bytes, at least 4)
+    // lies inside the frame (ip_fast_csum reads 4*ihl bytes for ihl >= 5, one
+    // dword for ihl <= 4: ps.h:68-70, pinned by oracle/ref/ub_probe.c)
     const bool ok14 = desc_ok && L >= 14;
     const bool isip = ok14 && eth == 0x0800u;
     const bool ok18 = isip && L >= 18;
     const bool shrt = !tx && ipl < 20;                                    // ip_in.c:25-26
-    const bool okhdr = ok18 && !shrt && L >= 14 + 4 * (ihl > 1 ? ihl : 1);
+    const bool okhdr = ok18 && !shrt && L >= 14 + 4 * (ihl > 4 ? ihl : 1);
     // ip_fast_csum: ihl <= 4 returns dword 0 as is (ps.h:72-73)
     const uint32_t s_ip = ipsum(ihl);
     const uint32_t ip_csum = ihl <= 4 ? (d0 >> 16) : fold_csum(s_ip);

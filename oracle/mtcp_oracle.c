@@ -217,7 +217,7 @@ int oracle_rx_packet(const uint8_t *pkt, uint32_t len, const oracle_rss_cfg *rss
     r->ihl_doff = (uint8_t)ihl;
     if (ip_len < 20)                                 /* ip_in.c:25-26 */
         VERDICT(MTCP_GPU_V_IP_SHORT);
-    NEED(14 + 4 * (ihl > 1 ? ihl : 1));              /* ps.h:68 reads >= 1 dword */
+    NEED(14 + 4 * (ihl > 4 ? ihl : 1));              /* ps.h:68-70: ihl <= 4 reads one dword */
     r->ip_csum = oracle_ip_fast_csum(pkt + 14, ihl); /* ip_in.c:35 */
     if (r->ip_csum)
         VERDICT(MTCP_GPU_V_IP_CSUM_BAD);

@@ -39,3 +39,72 @@ def test_rows_refuse_multi_gpu(bench, monkeypatch):
     monkeypatch.setattr("sys.argv", ["bench.py", "--config", "f1", "--gpus", "2"])
     with pytest.raises(SystemExit):
         bench.run_row(bench.parse())
+
+
+class _FakeRanks:
+    """Stands in for the launcher process: records the command, prints what
+    a 2-rank run prints (launcher chatter and rank 0's one JSON line)."""
+    seen = {}
+
+    def __init__(self, cmd, env=None, stdout=None, text=None, bufsize=None):
+        _FakeRanks.seen = dict(cmd=cmd, env=env)
+        self.stdout = iter(["launcher: starting 2 ranks\n", '{"metric": "m", "n_gpus": 2}\n'])
+
+    def wait(self):
+        return 0
+
+
+def test_self_launch_starts_n_ranks(bench, monkeypatch, capsys):
+    """`bench.py --gpus N` without WORLD_SIZE: the parent starts
+    torch.distributed.run with N ranks on 127.0.0.1 and a free port, the
+    same arguments, and forwards the ranks' single JSON line to stdout."""
+    import subprocess
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("MTCP_BENCH_DEVICE", "0")
+    monkeypatch.setattr(subprocess, "Popen", _FakeRanks)
+    argv = ["--gpus", "2", "--config", "c2", "--steps", "3"]
+    monkeypatch.setattr("sys.argv", ["bench.py", *argv])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0
+    cmd = _FakeRanks.seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "127.0.0.1" in cmd
+    port = [c for c in cmd if c.startswith("--master-port=")]
+    assert len(port) == 1 and 0 < int(port[0].split("=")[1]) < 65536
+    assert cmd[-len(argv):] == argv and cmd[-len(argv) - 1].endswith("bench.py")
+    assert _FakeRanks.seen["env"]["MASTER_ADDR"] == "127.0.0.1"
+    out, err = capsys.readouterr()
+    assert out.strip().splitlines() == ['{"metric": "m", "n_gpus": 2}']
+    assert "launcher: starting" in err
+
+
+def test_self_launch_fails_when_a_rank_fails(tmp_path):
+    """The real path end to end on a GPU-less host: the parent launches two
+    ranks (both pointed at device 0), they fail at their first GPU call, and
+    the parent exits non-zero without printing a JSON line."""
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present (tests/test_gpu_shard.py runs this path there)")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MTCP_BENCH_DEVICE"] = "0"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--per-gpu", "4096", "--cpu-baseline", "off", "--pcie", "off"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_self_launch_refuses_more_gpus_than_visible(tmp_path):
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.device_count() >= 64:
+        pytest.skip("64 GPUs visible")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MTCP_BENCH_DEVICE")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "64"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "GPU(s) visible" in p.stderr

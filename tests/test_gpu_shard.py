@@ -64,17 +64,28 @@ def test_c4_shard_two_launches(gpu, rank):
     assert_same(got[idx], oracle.rx_chunk(host, sh.desc[idx], 6), f"c4 shard {rank}")
 
 
-def _bench_ranks(tmp_path, config, per_gpu, world=2):
-    dump = tmp_path / config
-    env = dict(os.environ, MTCP_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
-    port = 29600 + os.getpid() % 300
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
-           "--gpus", str(world), "--config", config, "--per-gpu", str(per_gpu), "--steps", "3",
-           "--warmup", "1", "--cpu-baseline", "off", "--pcie", "off", "--dump-records", str(dump)]
+def _bench_ranks(tmp_path, config, per_gpu, world=2, launcher="torchrun"):
+    """bench.py's N-rank path.  launcher "torchrun": the driver's form
+    (python -m torch.distributed.run ... bench.py --gpus N); "self": plain
+    `python3 bench.py --gpus N`, which starts its own ranks (bench.py
+    self_launch) — WORLD_SIZE is removed from the environment."""
+    dump = tmp_path / f"{config}_{launcher}"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MTCP_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--config", config,
+            "--per-gpu", str(per_gpu), "--steps", "3", "--warmup", "1", "--cpu-baseline", "off",
+            "--pcie", "off", "--dump-records", str(dump)]
+    if launcher == "torchrun":
+        port = 29600 + os.getpid() % 300
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", *args]
+    else:
+        cmd = [sys.executable, *args]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
-    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    json_lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(json_lines) == 1, p.stdout[-2000:]
+    line = json.loads(json_lines[0])
     recs, metas = [], []
     for r in range(world):
         metas.append(json.load(open(dump / f"shard_rank{r}.json")))
@@ -82,10 +93,12 @@ def _bench_ranks(tmp_path, config, per_gpu, world=2):
     return line, metas, recs
 
 
-@pytest.mark.parametrize("config,size,rss,per_gpu", [("c2", 1500, False, 1 << 17),
-                                                     ("c3", "bimodal", True, 1 << 17)])
-def test_bench_two_ranks_equal_one_launch(gpu, tmp_path, config, size, rss, per_gpu):
-    line, metas, recs = _bench_ranks(tmp_path, config, per_gpu)
+@pytest.mark.parametrize("config,size,rss,per_gpu,launcher",
+                         [("c2", 1500, False, 1 << 17, "torchrun"),
+                          ("c3", "bimodal", True, 1 << 17, "torchrun"),
+                          ("c2", 1500, False, 1 << 17, "self")])
+def test_bench_two_ranks_equal_one_launch(gpu, tmp_path, config, size, rss, per_gpu, launcher):
+    line, metas, recs = _bench_ranks(tmp_path, config, per_gpu, launcher=launcher)
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["config"]["packets_total"] == 2 * per_gpu
     first = 0

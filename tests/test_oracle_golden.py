@@ -99,6 +99,85 @@ def test_rx_chunk_matches_reference(golden):
     assert branches == set(range(10))
 
 
+def _ub_probe(golden, name):
+    """oracle/ref/ub_probe.c's per-frame byte: bit 0 the reference faulted
+    with a PROT_NONE page right after the frame, bit 1 that fault was the
+    masked odd trailing byte of TCPCalcChecksum (tcp_util.c:175-176), bit 2
+    the reference read past len otherwise (ref-UB by observation)."""
+    import os
+    from tests.golden_io import GOLDEN
+    p = np.fromfile(os.path.join(GOLDEN, name), dtype=np.uint8)
+    assert len(p) == len(golden.desc)
+    return p
+
+
+def _segment_odd_at_len(golden, i):
+    o, n = int(golden.desc["offset"][i]), int(golden.desc["len"][i])
+    f = golden.buf[o:o + n].astype(np.int64)
+    ihl, tot = f[14] & 0xF, f[16] << 8 | f[17]
+    return 14 + tot == n and tot >= 4 * ihl and (tot - 4 * ihl) % 2 == 1
+
+
+def test_ref_ub_is_what_the_reference_reads_past_len(golden):
+    """The ref-UB set (golden_gen's, i.e. the oracle's TRUNCATED verdict) is
+    exactly the set of frames for which the REFERENCE's own code reads past
+    the frame: the reference's rx chain (compiled from /root/reference at -O0,
+    so that every load the source writes runs in the source's order) run on
+    each golden frame placed against a PROT_NONE guard page, under a SIGSEGV
+    handler (oracle/ref/ub_probe.c; regenerated by `make -C oracle golden`).
+    Reads: ip_fast_csum's 4*ihl bytes, one dword for ihl <= 4
+    (io_engine/include/ps.h:66-95), the header fields of eth_in.c:13,
+    ip_in.c:19-21 and tcp_in.c:1141-1149, TCPCalcChecksum's len bytes
+    (tcp_util.c:168-176).  The one read past len that is not UB — the masked
+    high byte of an odd segment's last word — is told apart by re-running
+    with one readable byte of four values after the frame."""
+    p = _ub_probe(golden, "rx_ub_probe.bin")
+    assert np.array_equal((p & 4) != 0, golden.meta["ref_ub"] == 1)
+    masked = np.nonzero(p & 2)[0]
+    assert len(masked) > 100                         # odd TCP segments ending at len
+    assert all(_segment_odd_at_len(golden, i) for i in masked)
+    assert set(golden.meta["branch"][masked].tolist()) <= {0, 9}
+    # the ICMP frames flagged 2 (icmp.c:31-33 reads an uninitialised byte of
+    # a local, not past the frame) do not fault
+    assert not (p[golden.meta["ref_ub"] == 2] & 4).any()
+
+
+def test_ref_ub_at_mtcp_build_flags(golden):
+    """The same probe through the reference built as mTCP builds it (-O3):
+    the reads past len are the -O0 set minus five TCP_LEN_BAD frames whose
+    20-byte TCP header passes the frame's end, where gcc sinks the tcph->seq
+    / ack_seq / window loads of the declarations (tcp_in.c:1147-1149) past
+    the length check (tcp_in.c:1155-1156) that makes them dead; and gcc's
+    byte load for the odd trailing word reads nothing past len."""
+    p0 = _ub_probe(golden, "rx_ub_probe.bin")
+    p3 = _ub_probe(golden, "rx_ub_probe_o3.bin")
+    ub0, ub3 = (p0 & 4) != 0, (p3 & 4) != 0
+    assert not (ub3 & ~ub0).any()
+    only0 = np.nonzero(ub0 & ~ub3)[0]
+    assert len(only0) == 5 and (golden.meta["branch"][only0] == 8).all()
+    for i in only0:
+        o, n = int(golden.desc["offset"][i]), int(golden.desc["len"][i])
+        ihl = int(golden.buf[o + 14]) & 0xF
+        assert 14 + 4 * ihl + 13 <= n < 14 + 4 * ihl + 16     # doff inside, window past
+    assert not (p3 & 2).any()
+
+
+def test_ub_probe_reproduces(golden, tmp_path):
+    """Where the reference build is present, re-run the probe: it writes the
+    committed bytes."""
+    import os
+    import subprocess
+    from tests.golden_io import GOLDEN
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for exe, name in (("ub_probe_O0", "rx_ub_probe.bin"), ("ub_probe", "rx_ub_probe_o3.bin")):
+        path = os.path.join(root, "oracle", "_ref", exe)
+        if not os.path.exists(path):
+            pytest.skip("oracle/_ref not built (needs /root/reference)")
+        out = tmp_path / name
+        subprocess.run([path, GOLDEN, str(out)], check=True, capture_output=True, timeout=300)
+        assert out.read_bytes() == open(os.path.join(GOLDEN, name), "rb").read()
+
+
 def test_rx_verdicts_match_reference_return_values(golden):
     """ProcessPacket's return (ERROR -1 / FALSE 0 / TRUE 1) against the verdict."""
     ok = golden.meta["ref_ub"] == 0
