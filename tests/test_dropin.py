@@ -1,0 +1,134 @@
+"""The drop-in at the reference's real call sites (b, f2).
+
+oracle/_ref/dropin_rx (oracle/ref/dropin_rx.c, built by `make -C oracle
+ref` from /root/reference) runs mTCP's own rx chain — eth_in.c / ip_in.c /
+tcp_in.c / tcp_util.c compiled WITHOUT -DDISABLE_HWCSUM — under the rx
+section of RunMainLoop (mtcp/src/core.c:763-777), with mtcp->iom =
+&gpu_module_func (mtcp_amd/io_module/gpu_module.c compiled against mTCP's
+real headers) wrapping a PSIO-like backend, over the golden chunk.  The
+expectation is the --disable-hwcsum reference's own outcome for every frame
+(tests/golden/, oracle/ref/golden_gen.c):
+
+* GPU: the reference asks dev_ioctl(PKT_RX_IP_CSUM) (ip_in.c:28-31) and
+  dev_ioctl(PKT_RX_TCP_CSUM) (tcp_in.c:1159-1164), gets 0 and never runs a
+  software checksum; the frames the --disable-hwcsum reference drops on a
+  checksum, and its ref-UB frames, come back NULL from get_rptr; every other
+  frame takes the reference's branch with the reference's return value and
+  stream key; nstat.rx_errors equals the --disable-hwcsum count (+ the ref-UB
+  frames).
+* no GPU (this container): dev_ioctl answers -1 and the reference computes
+  everything itself: every branch as with --disable-hwcsum.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+EXE = os.path.join(ROOT, "oracle", "_ref", "dropin_rx")
+REC = np.dtype([("served", "u1"), ("branch", "u1"), ("ret", "i1"), ("ioctl_ip", "i1"),
+                ("ioctl_tcp", "i1"), ("csum_called", "u1"), ("same", "u1"), ("pad", "u1"),
+                ("key", "u1", 12)])
+BR_TCP_OK, BR_IP_SHORT, BR_IP_CSUM_BAD, BR_TCP_LEN_BAD, BR_TCP_CSUM_BAD = 0, 3, 4, 8, 9
+NULL = 254
+
+
+def run_dropin(tmp_path, mode="observe", pipeline="1"):
+    if not os.path.exists(EXE):
+        pytest.fail("oracle/_ref/dropin_rx not built: `make -C oracle ref` (needs /root/reference)")
+    out = tmp_path / f"dropin_{mode}_{pipeline}.bin"
+    p = subprocess.run([EXE, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
+                        str(out), mode], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX="0"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1]), np.fromfile(out, dtype=REC)
+
+
+def golden_ret(golden):
+    return golden.meta["ret"].astype(np.int8) - 1     # golden_gen stores ret + 1
+
+
+def flow_keys(golden):
+    return np.fromfile(os.path.join(GOLD, "rx_flowkey.bin"), dtype=np.uint8).reshape(-1, 12)
+
+
+def test_dropin_passthrough_without_gpu(tmp_path, golden):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    if not os.path.exists(EXE):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    stats, r = run_dropin(tmp_path)
+    n = len(golden.desc)
+    ok = golden.meta["ref_ub"] == 0
+    assert stats["frames"] == stats["seen"] == stats["served"] == n and stats["null"] == 0
+    # no GPU: every asked dev_ioctl answers -1, so mTCP runs its own checks
+    assert set(np.unique(r["ioctl_ip"]).tolist()) == {-2, -1}
+    assert set(np.unique(r["ioctl_tcp"]).tolist()) == {-2, -1}
+    br = golden.meta["branch"]
+    assert np.array_equal(r["branch"][ok], br[ok])
+    assert np.array_equal(r["ret"][ok & (br != BR_TCP_OK)], golden_ret(golden)[ok & (br != BR_TCP_OK)])
+    sw = ok & np.isin(br, [BR_TCP_OK, BR_TCP_CSUM_BAD])
+    assert np.array_equal(r["csum_called"][ok] == 1, sw[ok])
+    tcp = ok & (br == BR_TCP_OK)
+    assert np.array_equal(r["key"][tcp], flow_keys(golden)[tcp])
+    assert stats["rx_errors"] == int((r["ret"] == -1).sum())
+    # a served frame differs from the original only where the reference, on
+    # the ref-UB frame before it, zeroed a tcph->check that lies past that
+    # frame (tcp_in.c:1171 with ihl pointing past len)
+    changed = np.nonzero(r["same"] == 0)[0]
+    assert all(i > 0 and golden.meta["ref_ub"][i - 1] == 1 for i in changed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,pipeline", [("observe", "1"), ("observe", "0"), ("plain", "1")])
+def test_dropin_at_the_reference_call_sites(tmp_path, golden, mode, pipeline):
+    stats, r = run_dropin(tmp_path, mode, pipeline)
+    n = len(golden.desc)
+    ub = golden.meta["ref_ub"] == 1
+    ok = ~ub
+    br = golden.meta["branch"]
+    assert stats["frames"] == stats["seen"] == n
+    # dropped by gpu_module (NULL from get_rptr): the reference's checksum
+    # drops (ip_in.c:35-36, tcp_in.c:1167-1173) and the frames it reads past
+    want_null = (ok & np.isin(br, [BR_IP_CSUM_BAD, BR_TCP_CSUM_BAD])) | ub
+    assert np.array_equal(r["branch"] == NULL, want_null)
+    assert stats["null"] == int(want_null.sum()) > 100
+    served = ~want_null
+    # every other frame: the reference's branch, return value and stream key
+    assert np.array_equal(r["branch"][served], br[served])
+    nok = served & (br != BR_TCP_OK)
+    assert np.array_equal(r["ret"][nok], golden_ret(golden)[nok])
+    tcp = served & (br == BR_TCP_OK)
+    assert tcp.sum() > 1000 and np.array_equal(r["key"][tcp], flow_keys(golden)[tcp])
+    # mTCP never ran a software TCP checksum
+    assert stats["tcp_csum_calls"] == 0 and not r["csum_called"].any()
+    # nstat.rx_errors: the --disable-hwcsum reference's error count over the
+    # defined frames, plus the ref-UB frames
+    want_err = int((ok & np.isin(br, [BR_IP_SHORT, BR_IP_CSUM_BAD, BR_TCP_LEN_BAD,
+                                      BR_TCP_CSUM_BAD])).sum()) + int(ub.sum())
+    assert stats["rx_errors"] == want_err
+    assert stats["changed"] == 0
+    if mode == "observe":
+        # ip_in.c:28-31 asked for every served IPv4 frame past the tot_len
+        # test, tcp_in.c:1159-1164 for every served frame past the TCP length
+        # test; every answer was 0
+        asked_ip = r["ioctl_ip"] != -2
+        asked_tcp = r["ioctl_tcp"] != -2
+        assert (r["ioctl_ip"][asked_ip] == 0).all() and (r["ioctl_tcp"][asked_tcp] == 0).all()
+        assert np.array_equal(asked_tcp, tcp)
+        v4_past_short = served & ~np.isin(br, [1, 2, BR_IP_SHORT])
+        assert np.array_equal(asked_ip, v4_past_short)
+    # a TCP frame whose tot_len runs past the frame is NULL (and
+    # counted in rx_errors); a frame with Ethernet padding after its datagram
+    # is served and checked
+    off = golden.desc["offset"].astype(np.int64)
+    ln = golden.desc["len"].astype(np.int64)
+    tot = (golden.buf[off + 16].astype(np.int64) << 8) | golden.buf[off + 17]
+    past = ub & (ln >= 54) & (14 + tot > ln)
+    padded = ok & (br == BR_TCP_OK) & (14 + tot < ln)
+    assert past.sum() >= 8 and (r["branch"][past] == NULL).all()
+    assert padded.sum() >= 30 and (r["branch"][padded] == BR_TCP_OK).all()
