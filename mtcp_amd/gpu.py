@@ -102,20 +102,22 @@ class Context:
     @contextlib.contextmanager
     def _ordered(self, stream):
         """The stream handle for one device call.  None: PyTorch's current
-        stream; when that is the legacy default stream, which the C-ABI
-        cannot name (NULL there means the context's own non-blocking
-        stream), the call is ordered by synchronizing before and after."""
+        stream OF THIS CONTEXT'S DEVICE (whatever device is current); when
+        that is the legacy default stream, which the C-ABI cannot name (NULL
+        there means the context's own non-blocking stream), the call is
+        ordered by synchronizing that device's default stream before and the
+        context's stream after."""
         if stream is not None:
             yield _stream_handle(stream)
             return
         import torch
-        cur = torch.cuda.current_stream()
+        cur = torch.cuda.current_stream(self.device)
         if cur.cuda_stream:
             yield cur.cuda_stream
             return
         cur.synchronize()
         yield None
-        torch.cuda.ExternalStream(lib().mtcp_gpu_stream(self._h)).synchronize()
+        torch.cuda.ExternalStream(lib().mtcp_gpu_stream(self._h), device=self.device).synchronize()
 
     def rx_chunk_dev(self, buf, desc, n: int, off_shift: int, out, stream=None) -> None:
         with self._ordered(stream) as st:

@@ -44,7 +44,8 @@
  * it in rx_packets / rx_bytes (eth_in.c:20-23) — as for dpdk_get_rptr's
  * NIC-verified drops.
  *
- * Transmit, with MTCP_GPU_TX=1 in the environment: dev_ioctl
+ * Transmit, with MTCP_GPU_TX=1 in the environment (psio or dpdk underneath;
+ * refused over netmap, whose get_wptr sends the previous frame): dev_ioctl
  * (PKT_TX_TCPIP_CSUM_PEEK / PKT_TX_TCPIP_CSUM) answers 0, so mTCP leaves
  * iph->check and tcph->check for the device; get_wptr records every frame
  * it hands out, and send_pkts fills the recorded frames' checksums on the
@@ -85,6 +86,19 @@
 
 /* the backend being wrapped (e.g. &ps_module_func or &dpdk_module_func) */
 io_module_func *gpu_inner_module;
+
+/* netmap's get_wptr transmits the PREVIOUS frame and hands out one reused
+ * buffer (netmap_get_wptr, netmap_module.c:139-151): a frame has left before
+ * send_pkts, where the tx fill runs.  The tx offload is refused over it.
+ * Weak: harnesses that link no netmap module leave it NULL. */
+extern io_module_func netmap_module_func __attribute__((weak));
+
+/* The wrapped backend hands out separate tx buffers and transmits them only
+ * in send_pkts (psio: psio_module.c:154-245, dpdk: dpdk_module.c:282-370). */
+static int gpu_tx_capable(const io_module_func *inner)
+{
+    return inner != NULL && inner != &netmap_module_func;
+}
 
 /* One receiving interface: two aggregates (pipelined; synchronous uses [0]). */
 struct gpu_ifq {
@@ -213,6 +227,10 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
         return;
     g->pipeline = !(pl && strcmp(pl, "0") == 0);
     g->tx = tx && strcmp(tx, "1") == 0;
+    if (g->tx && !gpu_tx_capable(gpu_inner_module)) {
+        TRACE_ERROR("gpu_module: MTCP_GPU_TX=1 refused: the wrapped backend sends from get_wptr\n");
+        g->tx = 0;
+    }
 
     ndev = mtcp_gpu_device_count();
     if (ndev <= 0 || mtcp_gpu_open(&g->gpu, ctx->cpu % ndev, NULL, 1, 0) != MTCP_GPU_OK ||

@@ -326,6 +326,7 @@ int main(int argc, char **argv)
                 changed += !r->same;
             } else {
                 r->branch = 254;
+                r->ioctl_ip = r->ioctl_tcp = -2;             /* ProcessPacket never ran */
                 mtcp->nstat.rx_errors[0]++;
                 nulls++;
             }

@@ -120,6 +120,10 @@ static uint8_t *fake_rptr(struct mtcp_thread_context *ctx, int ifidx, int index,
 static int32_t fake_select(struct mtcp_thread_context *ctx) { (void)ctx; return 0; }
 static void fake_destroy(struct mtcp_thread_context *ctx) { ctx->io_private_context = NULL; }
 
+/* RXLOOP_AS_NETMAP=1: the fake backend is registered as netmap_module_func
+ * (gpu_module.c refuses the tx offload over netmap) */
+io_module_func netmap_module_func;
+
 static io_module_func fake_module = {
     .load_module = fake_load, .init_handle = fake_init, .link_devices = fake_link,
     .release_pkt = fake_release, .get_wptr = fake_wptr, .send_pkts = fake_send,
@@ -324,6 +328,10 @@ int main(int argc, char **argv)
     }
 
     gpu_inner_module = &fake_module;
+    if (getenv("RXLOOP_AS_NETMAP") && strcmp(getenv("RXLOOP_AS_NETMAP"), "1") == 0) {
+        netmap_module_func = fake_module;
+        gpu_inner_module = &netmap_module_func;
+    }
     gpu_module_func.load_module();
     pthread_barrier_init(&g_start, NULL, (unsigned)threads);
     for (t = 0; t < threads; t++) {                   /* contiguous shards */

@@ -57,3 +57,30 @@ def test_no_gpu_no_fallback():
     from mtcp_amd._lib import MtcpGpuError
     with pytest.raises(MtcpGpuError):
         gpu.Context(0)
+
+
+def test_default_stream_is_the_contexts_device(monkeypatch):
+    """with stream=None a device call is ordered on PyTorch's
+    current stream of the CONTEXT's device, not of whatever device is current
+    (a context on device 1 must never be queued on device 0's stream)."""
+    import torch
+    from mtcp_amd import gpu
+    asked = []
+
+    class _S:
+        cuda_stream = 0xBEEF
+
+    def fake_current_stream(device=None):
+        asked.append(device)
+        return _S()
+
+    monkeypatch.setattr(torch.cuda, "current_stream", fake_current_stream)
+    ctx = object.__new__(gpu.Context)
+    ctx._h = ctypes.c_void_p()
+    ctx.device = 3
+    with ctx._ordered(None) as st:
+        assert st == 0xBEEF
+    assert asked == [3]
+    with ctx._ordered(0x1234) as st:                # an explicit stream is used as given
+        assert st == 0x1234
+    assert asked == [3]

@@ -33,12 +33,13 @@ def build_rxloop() -> str:
     return os.path.join(ROOT, "tests", "c", "rxloop")
 
 
-def run_rxloop(tmp_path, threads=1, pipeline="1", mode="verify", tx="0"):
+def run_rxloop(tmp_path, threads=1, pipeline="1", mode="verify", tx="0", as_netmap="0"):
     exe = build_rxloop()
     status = tmp_path / "status.bin"
     p = subprocess.run([exe, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
                         str(status), mode, str(threads)], capture_output=True, text=True,
-                       timeout=300, env=dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX=tx))
+                       timeout=300, env=dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX=tx,
+                                             RXLOOP_AS_NETMAP=as_netmap))
     assert p.returncode == 0, p.stderr
     return json.loads(p.stdout.strip().splitlines()[-1]), np.fromfile(status, dtype=np.uint8)
 
@@ -145,6 +146,17 @@ def test_gpu_module_fills_tx_checksums(tmp_path, golden, threads):
     assert stats["ioctl_tx"] == 0 and stats["sw_filled"] == 0
     assert stats["sent"] == stats["frames"] == len(golden.desc)
     assert stats["send_calls"] >= len(golden.desc) // 64
+    assert np.array_equal(sent, tx_expect(golden))
+
+
+@pytest.mark.gpu
+def test_gpu_module_refuses_tx_over_netmap(tmp_path, golden):
+    """netmap's get_wptr sends the previous frame and reuses one
+    buffer (netmap_module.c:139-151), so frames would leave before send_pkts
+    filled them: over netmap_module_func MTCP_GPU_TX=1 is refused, dev_ioctl
+    answers -1 and mTCP fills every frame itself."""
+    stats, sent = run_rxloop(tmp_path, mode="tx", tx="1", as_netmap="1")
+    assert stats["ioctl_tx"] == -1 and stats["sw_filled"] == golden.manifest["tx_filled"]
     assert np.array_equal(sent, tx_expect(golden))
 
 
