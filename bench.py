@@ -96,6 +96,9 @@ def parse():
                     help="packets per GPU (default: the config's; tests use smaller batches)")
     ap.add_argument("--dump-records", default=None,
                     help="directory: each rank writes its result records there")
+    ap.add_argument("--record", default="full", choices=["full", "compact"],
+                    help="rx result record: the 40 B mtcp_gpu_result (default, the headline) or "
+                         "the 16 B mtcp_gpu_result16 of a MTCP_GPU_F_COMPACT context")
     return ap.parse_args()
 
 
@@ -195,7 +198,7 @@ def pcie_inclusive(ctx, host_buf, desc, nbytes, world):
     from mtcp_amd import gpu
     gpu.host_register(host_buf)
     try:
-        out = np.zeros(len(desc), dtype=gpu.RESULT_DTYPE)
+        out = np.zeros(len(desc), dtype=ctx.result_dtype)
         gpu.host_register(out)
         try:
             ctx.rx_chunk(host_buf, desc, 6, out)   # warm-up (allocates stages)
@@ -261,7 +264,7 @@ def small_batch(ctx, dev, stream, n=4096, size=1500, launches=100, reps=5):
     frame_bytes = int(desc["len"].astype(np.int64).sum())
     return {"frames": n, "frame_size": size, "us_per_launch": round(us, 2),
             "GBs": round(frame_bytes / us / 1e3, 1), "gpkt_per_s": round(n / us / 1e3, 3),
-            "kernel": "mg::rx_wave_kernel (a wavefront per packet, 2-load trips)",
+            "kernel": "mg::" + ctx.last_kernel,
             "note": f"{launches} launches of mtcp_gpu_rx_chunk_dev captured in a HIP graph, "
                     f"HIP events over a replay, median of {reps}"}
 
@@ -489,11 +492,13 @@ def main():
     torch.cuda.set_stream(stream)
     d_buf = torch.empty(sh.nbytes, dtype=torch.uint8, device=dev)
     d_desc = torch.from_numpy(sh.desc.view(np.uint8).copy()).to(dev)
-    d_out = torch.empty(sh.count * 40, dtype=torch.uint8, device=dev)
+    compact = args.record == "compact"
+    rec_bytes = 16 if compact else 40
+    d_out = torch.empty(sh.count * rec_bytes, dtype=torch.uint8, device=dev)
     gpu.pktgen_dev(d_buf, d_desc, sh.count, 6, cfg["seed"], sh.first_index, stream=stream)
     frame_bytes = int(sh.desc["len"].astype(np.int64).sum())
 
-    ctx = gpu.Context(device, rss=cfg["rss"], rss_queues=8, rss_endian=True)
+    ctx = gpu.Context(device, rss=cfg["rss"], rss_queues=8, rss_endian=True, compact=compact)
     step = lambda: ctx.rx_chunk_dev(d_buf, d_desc, sh.count, 6, d_out, stream=stream)
 
     for _ in range(args.warmup):
@@ -551,13 +556,16 @@ def main():
     else:
         kern_ms_max = kern_ms
 
+    kernel = ctx.last_kernel                 # the kernel the timed launches dispatched
     # verdict summary of the last step (sanity: corruption rate ~1/1024 + 1/4096)
-    recs = d_out.view(-1, 40)
-    res = recs[:, 36].cpu().numpy()
+    recs = d_out.view(-1, rec_bytes)
+    v_at, pl_at = (14, 8) if compact else (36, 32)   # verdict, payload_len (include/mtcp_gpu.h)
+    res = recs[:, v_at].cpu().numpy()
     ok_frac = float((res == 0).mean())
     # TCP payload bytes (payload_len of the records, tcp_in.c:1144): the
     # metric's "payload GB/s" without the 54+ B of headers per frame
-    payload = int(recs[:, 32:34].contiguous().view(torch.int16).to(torch.int64).bitwise_and(0xFFFF).sum())
+    payload = int(recs[:, pl_at:pl_at + 2].contiguous().view(torch.int16).to(torch.int64)
+                  .bitwise_and(0xFFFF).sum())
     if args.dump_records:
         os.makedirs(args.dump_records, exist_ok=True)
         d_out.cpu().numpy().tofile(os.path.join(args.dump_records, f"records_rank{rank}.bin"))
@@ -605,7 +613,8 @@ def main():
         tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                              # C4's per-GPU step is two launches of C2's shape (1 M x 1500 B
                              # each): the per-launch figure is C2's
-                             f"traffic_{'c2' if args.config == 'c4' else args.config}.json")
+                             f"traffic_{'c2' if args.config == 'c4' else args.config}"
+                             f"{'_compact' if compact else ''}.json")
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             if tj.get("lib_sha256") == lib_sha256():
@@ -633,11 +642,12 @@ def main():
             "config": {"workload": args.config + ": " + cfg["desc"], "packets_per_gpu": per_gpu,
                        "packets_total": total_pkts, "frame_bytes_total": total_bytes,
                        "rss": cfg["rss"], "parallelism": f"batch split x{world} (no collective)",
-                       "launch": "hip_graph" if use_graph else "direct"},
+                       "launch": "hip_graph" if use_graph else "direct",
+                       "record": f"{rec_bytes} B ({'mtcp_gpu_result16, MTCP_GPU_F_COMPACT' if compact else 'mtcp_gpu_result'})"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_note,
-                         "kernel": "mg::rx_kernel", "avg_launch_ms": round(kern_ms_max, 5),
+                         "kernel": "mg::" + kernel, "avg_launch_ms": round(kern_ms_max, 5),
                          "algorithmic_bytes_per_launch": frame_bytes},
             "tcp_ok_fraction": round(ok_frac, 5),
         }

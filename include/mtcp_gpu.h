@@ -70,7 +70,7 @@
 extern "C" {
 #endif
 
-#define MTCP_GPU_ABI_VERSION 1
+#define MTCP_GPU_ABI_VERSION 2   /* 2: MTCP_GPU_F_COMPACT, mtcp_gpu_result16 */
 
 /* ---- error codes (negative returns) ----------------------------------- */
 #define MTCP_GPU_OK        0
@@ -93,6 +93,8 @@ extern "C" {
 #define MTCP_GPU_F_RSS           0x1u  /* compute rss_hash / rss_queue per packet */
 #define MTCP_GPU_F_RSS_ENDIAN    0x2u  /* GetRSSCPUCore endian fix (util/rss.c:161-162;
                                           mtcp/src/rss.c:96-99 endian_check) */
+#define MTCP_GPU_F_COMPACT       0x4u  /* rx writes 16 B mtcp_gpu_result16 records (below)
+                                          instead of the 40 B mtcp_gpu_result */
 
 /*
  * Packet descriptor of a contiguous chunk.  Layout-compatible with PSIO's
@@ -169,12 +171,37 @@ typedef struct mtcp_gpu_result {
     uint16_t eth_type;    /* 38 ntohs(ethh->h_proto)    eth_in.c:13            */
 } mtcp_gpu_result;
 
+/*
+ * Compact per-packet result, 16 B, for callers that act on the verdict (and
+ * the checksums / RSS queue) only — an io_module that answers get_rptr with
+ * the frame or NULL, as dpdk_get_rptr does on the NIC's one checksum bit
+ * (mtcp/src/dpdk_module.c:473-479).  Written instead of mtcp_gpu_result by a
+ * context opened with MTCP_GPU_F_COMPACT: the rx entry points' `out` /
+ * `d_out` then point to mtcp_gpu_result16[n] (cast to mtcp_gpu_result *).
+ * Every field equals the same-named field of the 40 B record.
+ */
+typedef struct mtcp_gpu_result16 {
+    uint32_t rss_hash;    /*  0 */
+    uint16_t ip_csum;     /*  4 */
+    uint16_t tcp_csum;    /*  6 */
+    uint16_t payload_len; /*  8 */
+    uint16_t ip_len;      /* 10 */
+    uint8_t  ihl_doff;    /* 12 */
+    uint8_t  tcp_flags;   /* 13 */
+    uint8_t  verdict;     /* 14 */
+    uint8_t  rss_queue;   /* 15 */
+} mtcp_gpu_result16;
+
 typedef struct mtcp_gpu_ctx mtcp_gpu_ctx;
 
 /* Library / device introspection. */
 int         mtcp_gpu_abi_version(void);
 const char *mtcp_gpu_strerror(int err);
 int         mtcp_gpu_device_count(void);
+/* PCI address "dddd:bb:dd.f" of HIP device `device` (hipDeviceGetPCIBusId),
+ * for NUMA placement: an mTCP thread opens the device on its core's node, as
+ * mTCP binds a thread's memory to that node (mtcp/src/cpu.c:54-79). */
+int         mtcp_gpu_device_pci_bus_id(int device, char *buf, int len);
 
 /*
  * Open a context on HIP device `device`.
@@ -203,6 +230,15 @@ int  mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp);
 
 /* The HIP stream the context launches on (a hipStream_t, as void*). */
 void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx);
+
+/* Bytes per rx result record this context writes: 40, or 16 with
+ * MTCP_GPU_F_COMPACT; 0 for a NULL context. */
+uint32_t mtcp_gpu_record_size(const mtcp_gpu_ctx *ctx);
+
+/* Name of the kernel the context's last rx / tx launch dispatched (the
+ * schedule chosen by batch size and average slot), for profiles and bench
+ * lines; "" before the first launch. */
+const char *mtcp_gpu_last_kernel(const mtcp_gpu_ctx *ctx);
 
 /*
  * Device-resident rx: chunk, descriptors and results are device (or
@@ -292,6 +328,8 @@ int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_
 #define MTCP_GPU_FLOW_NONE       0xFFFFFFFFu  /* packet never reaches the flow table */
 
 /*
+ * (Both flow_hash entry points read 40 B records: a MTCP_GPU_F_COMPACT
+ * context answers MTCP_GPU_EINVAL; use the fused rx_*_flow_dev calls.)
  * Flow-table bin of every rx result: HashFlow (mtcp/src/tcp_stream.c:56-90,
  * Jenkins one-at-a-time over signed chars, masked to NUM_BINS_FLOWS - 1) of
  * the stream key ProcessTCPPacket hands to StreamHTSearch

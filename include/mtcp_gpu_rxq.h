@@ -76,8 +76,11 @@ int  mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q);
 int  mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n);
 
 /* get_rptr for flushed frame i: the staged frame and its length, or NULL for
- * the verdicts listed above.  *res (may be NULL) receives the
- * frame's full result record. */
+ * the verdicts listed above.  *res (may be NULL) receives the frame's result
+ * record: a mtcp_gpu_result, or — when the rxq's context was opened with
+ * MTCP_GPU_F_COMPACT (mtcp_gpu_record_size 16) — a mtcp_gpu_result16, cast.
+ * A compact context moves 16 B per frame back instead of 40 (gpu_module.c's
+ * rxqs read the verdict only). */
 uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
                           const mtcp_gpu_result **res);
 

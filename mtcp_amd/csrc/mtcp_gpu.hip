@@ -53,6 +53,7 @@ struct mtcp_gpu_ctx {
     uint64_t h_gather_cap = 0;
     mtcp_gpu_desc *h_gather_desc = nullptr;
     uint32_t h_gather_desc_cap = 0;
+    const char *last_kernel = "";                // mtcp_gpu_last_kernel
 };
 
 namespace {
@@ -149,7 +150,7 @@ constexpr uint64_t kLineAlignAboveSlotBytes = 1536;
 template <int SCHED, bool LALIGN>
 constexpr int prio_for() { return SCHED == mg::kSchedUnrolled && !LALIGN ? 5 : 0; }
 
-template <int MODE, bool RSS, int SCHED, bool LALIGN>
+template <int MODE, bool RSS, int SCHED, bool LALIGN, bool CMP>
 void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
     // tx fill streams its frames through L2 normally (NT off): its check-field
     // writes at the end then find part of the last passes' lines resident
@@ -160,7 +161,7 @@ void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
     // (C5: 4.768 -> 4.737 GB per launch = chunk + descriptors, no line twice)
     constexpr bool kRev = LALIGN && SCHED == mg::kSchedUnrolled;
     hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, SCHED, LALIGN, 0, 8, 8, kNT, 6, kRev, false,
-                                      prio_for<SCHED, LALIGN>()>),
+                                      prio_for<SCHED, LALIGN>(), mg::kWavesPerBlock, 0, CMP>),
                        grid, block, 0, st, kp);
 }
 
@@ -172,24 +173,28 @@ void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
 // frames keep the unrolled, line-aligned rounds at every size.
 constexpr uint32_t kSortedUpToPkts = 1u << 16;
 
-template <int MODE, bool RSS>
-void launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, uint64_t slot,
-                  uint32_t batch_n) {
+template <int MODE, bool RSS, bool CMP>
+const char *launch_sched(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp, uint64_t slot,
+                         uint32_t batch_n) {
     if constexpr (MODE == mg::kRxPtrs) {
         // pointer bursts carry no size hint the host can see (the lengths are
         // in device memory): the size-sorted rounds are the robust choice —
         // C3-shaped bursts 135.5 vs 162.1 us unrolled, C2-shaped 250.5 vs
         // 245.3, C5-shaped 687.7 vs 685.2 (tools/rx_variants ptrs_*)
-        launch_one<MODE, RSS, mg::kSchedSorted, true>(grid, block, st, kp);
+        launch_one<MODE, RSS, mg::kSchedSorted, true, CMP>(grid, block, st, kp);
+        return "rx_kernel<sorted,line-aligned>";
     } else {
         // the schedule is chosen once per batch (batch_n: the whole batch,
         // not this launch's share of it)
-        if (slot < kUnrollBelowSlotBytes || (batch_n <= kSortedUpToPkts && slot <= kLineAlignAboveSlotBytes))
-            launch_one<MODE, RSS, mg::kSchedSorted, false>(grid, block, st, kp);
-        else if (slot > kLineAlignAboveSlotBytes)
-            launch_one<MODE, RSS, mg::kSchedUnrolled, true>(grid, block, st, kp);
-        else
-            launch_one<MODE, RSS, mg::kSchedUnrolled, false>(grid, block, st, kp);
+        if (slot < kUnrollBelowSlotBytes || (batch_n <= kSortedUpToPkts && slot <= kLineAlignAboveSlotBytes)) {
+            launch_one<MODE, RSS, mg::kSchedSorted, false, CMP>(grid, block, st, kp);
+            return "rx_kernel<sorted>";
+        } else if (slot > kLineAlignAboveSlotBytes) {
+            launch_one<MODE, RSS, mg::kSchedUnrolled, true, CMP>(grid, block, st, kp);
+            return "rx_kernel<unrolled,line-aligned>";
+        }
+        launch_one<MODE, RSS, mg::kSchedUnrolled, false, CMP>(grid, block, st, kp);
+        return "rx_kernel<unrolled>";
     }
 }
 
@@ -249,23 +254,30 @@ int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_on
 constexpr uint64_t kWaveShortUpToSlot = 2048;
 
 template <int MODE, bool RSS>
-void launch_small(int sched, uint32_t n, uint64_t slot, hipStream_t st, const mg::KParams &kp) {
+const char *launch_small(int sched, uint32_t n, uint64_t slot, hipStream_t st, const mg::KParams &kp) {
     if (sched == kSchedWave) {
         const dim3 grid((n + mg::kWavesPerBlock - 1) / mg::kWavesPerBlock);
-        if (slot <= kWaveShortUpToSlot)
+        if (slot <= kWaveShortUpToSlot) {
             hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS, 0, 1, 2>), grid, dim3(mg::kBlock), 0, st, kp);
-        else
-            hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS>), grid, dim3(mg::kBlock), 0, st, kp);
+            return "rx_wave_kernel<2 loads>";
+        }
+        hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS>), grid, dim3(mg::kBlock), 0, st, kp);
+        return "rx_wave_kernel<10 loads>";
     } else if (sched == kSchedQuad) {
         constexpr uint32_t P = mg::GroupShape<4>::P;
         hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 4>), dim3((n + P - 1) / P), dim3(mg::kGroupBlock), 0,
                            st, kp);
-    } else {
-        constexpr uint32_t P = mg::GroupShape<16>::P;
-        hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 16>), dim3((n + P - 1) / P), dim3(mg::kGroupBlock), 0,
-                           st, kp);
+        return "rx_group_kernel<quad>";
     }
+    constexpr uint32_t P = mg::GroupShape<16>::P;
+    hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 16>), dim3((n + P - 1) / P), dim3(mg::kGroupBlock), 0,
+                       st, kp);
+    return "rx_group_kernel<row>";
 }
+
+// bytes per rx record: 40 (mtcp_gpu_result) or 16 (mtcp_gpu_result16)
+uint64_t record_size(const mg::KParams &kp) { return kp.compact ? 16 : 40; }
+uint64_t record_size(const mtcp_gpu_ctx *ctx) { return (ctx->flags & MTCP_GPU_F_COMPACT) ? 16 : 40; }
 
 template <int MODE>
 int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
@@ -275,10 +287,8 @@ int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     const uint64_t avg_slot = ptrs ? 1024 : kp.buf_len / kp.n;
     const int sched = pick_sched(ctx, kp.n, avg_slot, MODE == mg::kTxPtrs || kp.tx_report != nullptr);
     if (sched != kSchedBig) {
-        if (rss)
-            launch_small<MODE, true>(sched, kp.n, avg_slot, st, kp);
-        else
-            launch_small<MODE, false>(sched, kp.n, avg_slot, st, kp);
+        ctx->last_kernel = rss ? launch_small<MODE, true>(sched, kp.n, avg_slot, st, kp)
+                               : launch_small<MODE, false>(sched, kp.n, avg_slot, st, kp);
         return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
     }
     if constexpr (MODE != mg::kTxPtrs) {
@@ -294,12 +304,19 @@ int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
         } else {
             sub.desc = kp.desc + first;
         }
-        if (MODE != mg::kTxChunk) sub.out = kp.out + first;
+        if (MODE != mg::kTxChunk)
+            sub.out = reinterpret_cast<mtcp_gpu_result *>(reinterpret_cast<uint8_t *>(kp.out) +
+                                                          (uint64_t)first * record_size(kp));
         if (kp.bins) sub.bins = kp.bins + first;
-        if (rss)
-            launch_sched<MODE, true>(grid, block, st, sub, slot, kp.n);
-        else
-            launch_sched<MODE, false>(grid, block, st, sub, slot, kp.n);
+        if constexpr (mg::is_tx(MODE)) {
+            ctx->last_kernel = launch_sched<MODE, false, false>(grid, block, st, sub, slot, kp.n);
+        } else if (kp.compact) {
+            ctx->last_kernel = rss ? launch_sched<MODE, true, true>(grid, block, st, sub, slot, kp.n)
+                                   : launch_sched<MODE, false, true>(grid, block, st, sub, slot, kp.n);
+        } else {
+            ctx->last_kernel = rss ? launch_sched<MODE, true, false>(grid, block, st, sub, slot, kp.n)
+                                   : launch_sched<MODE, false, false>(grid, block, st, sub, slot, kp.n);
+        }
     }
     }
     return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
@@ -311,8 +328,13 @@ mg::KParams base_params(mtcp_gpu_ctx *ctx) {
     kp.rss_nq = ctx->rss_nq;
     kp.rss_endian = ctx->rss_endian;
     for (int i = 0; i < 4; ++i) kp.rss_key[i] = ctx->rss_key_w[i];
+    kp.compact = (ctx->flags & MTCP_GPU_F_COMPACT) ? 1u : 0u;
     return kp;
 }
+
+// results of the device entry points: 8 B aligned (40 B records, stored in
+// 8 and 16 B pieces), 16 B aligned for the compact records (one 16 B store)
+uintptr_t out_align(const mtcp_gpu_ctx *ctx) { return (ctx->flags & MTCP_GPU_F_COMPACT) ? 15 : 7; }
 
 hipStream_t pick(mtcp_gpu_ctx *ctx, void *stream) {
     return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
@@ -377,6 +399,13 @@ int mtcp_gpu_device_count(void) {
     int n = 0;
     if (!HIP_OK(hipGetDeviceCount(&n))) return 0;
     return n;
+}
+
+int mtcp_gpu_device_pci_bus_id(int device, char *buf, int len) {
+    if (!buf || len < 13) return MTCP_GPU_EINVAL;
+    int ndev = 0;
+    if (!HIP_OK(hipGetDeviceCount(&ndev)) || device < 0 || device >= ndev) return MTCP_GPU_ENODEV;
+    return HIP_OK(hipDeviceGetPCIBusId(buf, len, device)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
 
 int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rss_num_queues,
@@ -501,6 +530,10 @@ int mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp) {
 
 void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+uint32_t mtcp_gpu_record_size(const mtcp_gpu_ctx *ctx) { return ctx ? (uint32_t)record_size(ctx) : 0u; }
+
+const char *mtcp_gpu_last_kernel(const mtcp_gpu_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
+
 int mtcp_gpu_sync(mtcp_gpu_ctx *ctx) {
     if (!ctx) return MTCP_GPU_EINVAL;
     DeviceGuard dg(ctx->device);
@@ -511,7 +544,7 @@ int mtcp_gpu_rx_chunk_flow_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t bu
                                const mtcp_gpu_desc *d_desc, uint32_t n, uint32_t off_shift,
                                mtcp_gpu_result *d_out, uint32_t *d_bins, void *stream) {
     if (!ctx || (n && (!d_buf || !d_desc || !d_out)) || off_shift > 16 || (buf_len & 15) ||
-        ((uintptr_t)d_buf & 15) || ((uintptr_t)d_out & 7) || ((uintptr_t)d_desc & 7) ||
+        ((uintptr_t)d_buf & 15) || ((uintptr_t)d_out & out_align(ctx)) || ((uintptr_t)d_desc & 7) ||
         ((uintptr_t)d_bins & 3))
         return MTCP_GPU_EINVAL;
     DeviceGuard dg(ctx->device);
@@ -534,7 +567,7 @@ int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len
 
 int mtcp_gpu_rx_ptrs_flow_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts, const uint16_t *d_lens,
                               uint32_t n, mtcp_gpu_result *d_out, uint32_t *d_bins, void *stream) {
-    if (!ctx || (n && (!d_pkts || !d_lens || !d_out)) || ((uintptr_t)d_out & 7) ||
+    if (!ctx || (n && (!d_pkts || !d_lens || !d_out)) || ((uintptr_t)d_out & out_align(ctx)) ||
         ((uintptr_t)d_bins & 3))
         return MTCP_GPU_EINVAL;
     DeviceGuard dg(ctx->device);
@@ -590,6 +623,8 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
     int rc = MTCP_GPU_OK;
+    uint8_t *const out_b = reinterpret_cast<uint8_t *>(out);
+    const size_t rec = (size_t)record_size(ctx);
     if (!offsets_sorted(desc, n)) {
         // arbitrary order: stage the whole chunk once, then batches of descriptors
         Stage &s = ctx->stage[0];
@@ -611,7 +646,7 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
                 rc = MTCP_GPU_EIO;
             if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream);
             if (rc == MTCP_GPU_OK &&
-                !HIP_OK(hipMemcpyAsync(out + first, s.d_out, (size_t)cnt * sizeof(mtcp_gpu_result),
+                !HIP_OK(hipMemcpyAsync(out_b + first * rec, s.d_out, cnt * rec,
                                        hipMemcpyDeviceToHost, s.stream)))
                 rc = MTCP_GPU_EIO;
         }
@@ -649,7 +684,7 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
                 rc = MTCP_GPU_EIO;
             if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream);
             if (rc == MTCP_GPU_OK &&
-                !HIP_OK(hipMemcpyAsync(out + first, s.d_out, (size_t)cnt * sizeof(mtcp_gpu_result),
+                !HIP_OK(hipMemcpyAsync(out_b + first * rec, s.d_out, cnt * rec,
                                        hipMemcpyDeviceToHost, s.stream)))
                 rc = MTCP_GPU_EIO;
             first += cnt;
@@ -804,7 +839,8 @@ int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mt
 // ---- flow-table hash --------------------------------------
 int mtcp_gpu_flow_hash_dev(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *d_res, uint32_t n,
                            uint32_t *d_bins, void *stream) {
-    if (!ctx || (n && (!d_res || !d_bins)) || ((uintptr_t)d_res & 7) || ((uintptr_t)d_bins & 3))
+    if (!ctx || (n && (!d_res || !d_bins)) || ((uintptr_t)d_res & 7) || ((uintptr_t)d_bins & 3) ||
+        (ctx->flags & MTCP_GPU_F_COMPACT))          // reads 40 B records (the 4-tuple)
         return MTCP_GPU_EINVAL;
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
@@ -817,7 +853,7 @@ int mtcp_gpu_flow_hash_dev(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *d_res, uint
 
 int mtcp_gpu_flow_hash(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *res, uint32_t n,
                        uint32_t *bins) {
-    if (!ctx || (n && (!res || !bins))) return MTCP_GPU_EINVAL;
+    if (!ctx || (n && (!res || !bins)) || (ctx->flags & MTCP_GPU_F_COMPACT)) return MTCP_GPU_EINVAL;
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
     Stage &s = ctx->stage[0];

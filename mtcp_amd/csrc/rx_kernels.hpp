@@ -24,7 +24,7 @@
 //            checksum), subtracts from the chunk sum the bytes outside the
 //            TCP segment [T, E) (E = 14 + tot_len), adds the pseudo header,
 //            folds, hashes the 4-tuple through 24 nibble tables in LDS and
-//            holds its 40 B record in registers; the held records of up to
+//            holds its 40 B record (16 B with CMP) in registers; the held records of up to
 //            8 passes are stored at the end (through LDS, as 16 B pieces of
 //            contiguous runs) — stores interleaved with the frame stream
 //            cost several times their bytes.
@@ -53,7 +53,8 @@ constexpr int kSlotChunks = 8;           // chunks 0..6 raw (headers), 7 = last 
 constexpr int kRow = 16;                 // lanes per DPP row = lanes per frame
 constexpr int kUnroll = 6;               // loads in flight per row (96 chunks = 1536 B)
 
-// kTxPtrs (tx fill of a pointer burst) runs in rx_wave_kernel only.
+// kTxPtrs (tx fill of a pointer burst) and the tx report run in the small
+// kernels only (rx_wave_kernel, rx_group_kernel: mtcp_gpu.hip pick_sched).
 enum Mode : int { kRxChunk = 0, kRxPtrs = 1, kTxChunk = 2, kTxPtrs = 3 };
 constexpr bool is_tx(int m) { return m == kTxChunk || m == kTxPtrs; }
 // Phase-1 schedules (rx_kernel's SCHED; see its comment).  Dispatched:
@@ -84,6 +85,7 @@ struct KParams {
     uint2 *tx_report;              // tx (wave kernel): {checks, T} per frame instead of writing them
     uint32_t *stamps;              // profiling builds only (rx_kernel STAMP): 4 dwords per wave
     uint32_t rss_key[4];           // key bytes 0..15, big-endian words (wave kernel's Toeplitz)
+    uint32_t compact;              // rx: 16 B mtcp_gpu_result16 records (MTCP_GPU_F_COMPACT)
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -590,6 +592,33 @@ __device__ __forceinline__ void pack_record(const Pkt &k, uint32_t rss_hash, uin
     r[9] = k.verdict | (rss_queue << 8) | (k.eth_type << 16);
 }
 
+// The 16 B record (mtcp_gpu_result16, MTCP_GPU_F_COMPACT) as four dwords:
+// the same fields as pack_record's, for callers that need the verdict only.
+__device__ __forceinline__ void pack_compact(const Pkt &k, uint32_t rss_hash, uint32_t rss_queue,
+                                             uint32_t (&r)[4]) {
+    r[0] = rss_hash;
+    r[1] = k.ip_csum | (k.tcp_csum << 16);
+    r[2] = k.payload_len | (k.ip_len << 16);
+    r[3] = k.ihl_doff | (k.flags << 8) | (k.verdict << 16) | (rss_queue << 24);
+}
+
+// Store one packet's record from one lane (the small kernels' per-lane phase
+// 2): 40 B as five 8 B pieces, or 16 B as one piece.
+__device__ __forceinline__ void store_record(const KParams &kp, uint32_t rec, const Pkt &k,
+                                             uint32_t rss_hash, uint32_t rss_queue) {
+    if (kp.compact) {
+        uint32_t c[4];
+        pack_compact(k, rss_hash, rss_queue, c);
+        reinterpret_cast<uint4 *>(kp.out)[rec] = make_uint4(c[0], c[1], c[2], c[3]);
+    } else {
+        uint32_t r[10];
+        pack_record(k, rss_hash, rss_queue, r);
+        uint2 *o = reinterpret_cast<uint2 *>(kp.out + rec);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) o[i] = make_uint2(r[2 * i], r[2 * i + 1]);
+    }
+}
+
 // util/rss.c:107-145 as 24 nibble tables (built on the host from the key
 // cache of BuildKeyCache, util/rss.c:13-105): the input bytes (sip, dip, sp,
 // dp host order, MSB first) are saddr / daddr / ports in memory order.
@@ -674,9 +703,12 @@ struct Trip {
 // s_setprio(PRIO & 3): the older wave of a SIMD otherwise wins its issue
 // arbitration and finishes first; PRIO & 4: only for the first half of its
 // passes.
+// CMP: write 16 B mtcp_gpu_result16 records (MTCP_GPU_F_COMPACT) — four dwords
+// held per pass instead of ten, plus the flow bin when one is asked for (the
+// compact record has no 4-tuple to hash at the flush).
 template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
           bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0,
-          int WPB = kWavesPerBlock, int XSKIP = 0>
+          int WPB = kWavesPerBlock, int XSKIP = 0, bool CMP = false>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
     uint64_t t_start = 0;
     if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
@@ -922,46 +954,51 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))
     };
 
     constexpr int kDefer = MODE == kTxChunk ? 0 : DEFER;
-    uint32_t keep[kDefer > 0 ? kDefer : 1][10];   // keep[q]: the record of q passes ago
+    // record dwords stored per packet (RW) and held per packet (HW: the
+    // compact record also holds its flow bin)
+    constexpr int RW = CMP ? 4 : 10, HW = CMP ? 5 : 10;
+    uint32_t keep[kDefer > 0 ? kDefer : 1][HW];   // keep[q]: the record of q passes ago
     uint32_t held = 0;                            // passes in keep[] (wave-uniform)
     uint32_t last_g0 = 0;                         // pass base of keep[0]
+    uint8_t *const out_b = reinterpret_cast<uint8_t *>(kp.out);
     // Store the held records (lane k's record of pass last_g0 - q*pass_pkts).
     // Each pass's 64 records go through this wave's LDS so that the stores
-    // are 16 B pieces of the contiguous runs of B packets (B*40 bytes each):
+    // are 16 B pieces of the contiguous runs of B packets (B*RW*4 bytes each):
     // measured 8 us faster on C2 than every lane storing its own 40 B.
     auto flush = [&]() {
         if constexpr (kDefer > 0) {
             static_assert(B % 2 == 0, "16 B pieces need runs of an even number of records");
-            constexpr uint32_t kRunDw = B * 10, kRunPieces = kRunDw / 4;
+            constexpr uint32_t kRunDw = B * RW, kRunPieces = kRunDw / 4;
             uint32_t *stg = reinterpret_cast<uint32_t *>(&wl.hd[0]);
 #pragma unroll
             for (int q = 0; q < kDefer; ++q) {
                 if ((uint32_t)q < held) {
                     const uint32_t gq = last_g0 - (uint32_t)q * pass_pkts;
-                    uint2 *st = reinterpret_cast<uint2 *>(stg) + lane * 5;
+                    uint2 *st = reinterpret_cast<uint2 *>(stg) + lane * (RW / 2);
 #pragma unroll
-                    for (int i = 0; i < 5; ++i) st[i] = make_uint2(keep[q][2 * i], keep[q][2 * i + 1]);
+                    for (int i = 0; i < RW / 2; ++i) st[i] = make_uint2(keep[q][2 * i], keep[q][2 * i + 1]);
 #pragma unroll
-                    for (uint32_t pc = lane; pc < kWave * 10 / 4; pc += kWave) {
+                    for (uint32_t pc = lane; pc < kWave * RW / 4; pc += kWave) {
                         const uint32_t run = pc / kRunPieces, w = pc % kRunPieces;
                         const uint32_t first = gq + map(run * B);      // runs: B consecutive packets
-                        const uint32_t r0 = first + (4 * w) / 10, r1 = first + (4 * w + 2) / 10;
+                        const uint32_t r0 = first + (4 * w) / RW, r1 = first + (4 * w + 2) / RW;
                         const uint4 v = *reinterpret_cast<const uint4 *>(stg + run * kRunDw + 4 * w);
-                        uint8_t *dst = reinterpret_cast<uint8_t *>(kp.out + first) + 16 * w;
+                        uint8_t *dst = out_b + (uint64_t)first * (4 * RW) + 16 * w;
                         if (r1 < kp.n) {
                             *reinterpret_cast<uint4 *>(dst) = v;
                         } else if (r0 < kp.n) {                        // tail: half a piece
                             *reinterpret_cast<uint2 *>(dst) = make_uint2(v.x, v.y);
                         }
                     }
-                    // f3 fused: the flow-table bin of each held record, computed
-                    // from the record itself (no register held for it), stored
-                    // in runs of B consecutive packets
+                    // f3 fused: the flow-table bin of each held record (40 B:
+                    // computed from the record itself, no register held for
+                    // it; 16 B: held beside it), stored in runs of B packets
                     if (kp.bins) {
                         bool live;
                         const uint32_t rec = lane_pkt(gq, live);
                         if (live)
-                            kp.bins[rec] = flow_bin(keep[q][0], keep[q][1], keep[q][2], keep[q][9] & 0xFFu);
+                            kp.bins[rec] = CMP ? keep[q][HW - 1]
+                                               : flow_bin(keep[q][0], keep[q][1], keep[q][2], keep[q][9] & 0xFFu);
                     }
                 }
             }
@@ -970,15 +1007,15 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))
     };
 
     // hold this pass's record (flushing first when the buffer is full)
-    auto push = [&](const uint32_t (&r)[10], uint32_t g0) {
+    auto push = [&](const uint32_t (&r)[HW], uint32_t g0) {
         if constexpr (kDefer > 0) {
             if (held == (uint32_t)kDefer) flush();
 #pragma unroll
             for (int q = kDefer - 1; q > 0; --q)
 #pragma unroll
-                for (int i = 0; i < 10; ++i) keep[q][i] = keep[q - 1][i];
+                for (int i = 0; i < HW; ++i) keep[q][i] = keep[q - 1][i];
 #pragma unroll
-            for (int i = 0; i < 10; ++i) keep[0][i] = r[i];
+            for (int i = 0; i < HW; ++i) keep[0][i] = r[i];
             last_g0 = g0;
             ++held;
         }
@@ -1224,7 +1261,8 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))
 
         if constexpr (ABL >= 1) {
             if constexpr (kDefer > 0) {
-                const uint32_t r[10] = {wl.sum[lane], 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                uint32_t r[HW] = {};
+                r[0] = wl.sum[lane];
                 push(r, g0);
             } else if (live && wl.sum[lane] == 0x12345678u) {   // profiling: no stores
                 kp.out[k].saddr = wl.sum[lane];
@@ -1257,25 +1295,35 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))
                 tx_write(fill);
             }
         } else {
-            uint32_t r[10];
-            pack_record(pk, rss_hash, rss_queue, r);
+            uint32_t r[HW];
+            if constexpr (CMP) {
+                uint32_t c[4];
+                pack_compact(pk, rss_hash, rss_queue, c);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) r[i] = c[i];
+                r[4] = kp.bins ? flow_bin(pk.saddr, pk.daddr, pk.ports, pk.verdict) : 0u;
+            } else {
+                pack_record(pk, rss_hash, rss_queue, r);
+            }
             if constexpr (kDefer > 0) {
                 push(r, g0);
             } else {
-                // stage the 64 records (2560 B) in this wave's LDS, then store
-                // them as 8-byte pieces: lanes of one run of B packets write one
-                // contiguous B*40-byte span of the output
-                uint2 *st = reinterpret_cast<uint2 *>(wl.hd) + lane * 5;
+                // stage the 64 records (64 x RW dwords) in this wave's LDS,
+                // then store them as 8-byte pieces: lanes of one run of B
+                // packets write one contiguous span of the output
+                uint2 *st = reinterpret_cast<uint2 *>(wl.hd) + lane * (RW / 2);
 #pragma unroll
-                for (int i = 0; i < 5; ++i) st[i] = make_uint2(r[2 * i], r[2 * i + 1]);
+                for (int i = 0; i < RW / 2; ++i) st[i] = make_uint2(r[2 * i], r[2 * i + 1]);
                 const uint2 *src = reinterpret_cast<const uint2 *>(wl.hd);
 #pragma unroll
-                for (uint32_t i = 0; i < 5; ++i) {
-                    const uint32_t q = i * kWave + lane;      // 8-byte piece of record q/5
-                    const uint32_t rec = g0 + map(q / 5);
-                    if (rec < kp.n) reinterpret_cast<uint2 *>(kp.out + rec)[q % 5] = src[q];
+                for (uint32_t i = 0; i < RW / 2; ++i) {
+                    const uint32_t q = i * kWave + lane;      // 8-byte piece of record q / (RW / 2)
+                    const uint32_t rec = g0 + map(q / (RW / 2));
+                    if (rec < kp.n)
+                        reinterpret_cast<uint2 *>(out_b + (uint64_t)rec * (4 * RW))[q % (RW / 2)] = src[q];
                 }
-                if (kp.bins && live) kp.bins[k] = flow_bin(r[0], r[1], r[2], r[9] & 0xFFu);
+                if (kp.bins && live)
+                    kp.bins[k] = CMP ? r[HW - 1] : flow_bin(r[0], r[1], r[2], r[9] & 0xFFu);
             }
         }
     }

@@ -29,7 +29,8 @@
 //            64 + i, the key window of each bit comes straight from the key
 //            words (BuildKeyCache, util/rss.c:13-105, without the table), an
 //            XOR reduction finishes it — so no table is staged per workgroup.
-//   stores   lanes 0..4 write the 40 B record as five 8 B pieces; the tx fill
+//   stores   lanes 0..4 write the 40 B record as five 8 B pieces (lanes 0..1
+//            the 16 B compact record, MTCP_GPU_F_COMPACT); the tx fill
 //            writes its two 16-bit check fields from lane 0.
 #pragma once
 
@@ -286,16 +287,24 @@ __global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
                 rss_queue = rss_core(rss_hash, kp.rss_nq, kp.rss_endian);
             }
         }
-        uint32_t r[10];
-        pack_record(pk, rss_hash, rss_queue, r);
-        if (lane < 5) {
-            uint32_t xx = r[0], yy = r[1];
+        if (kp.compact) {
+            uint32_t c[4];
+            pack_compact(pk, rss_hash, rss_queue, c);
+            if (lane < 2)
+                reinterpret_cast<uint2 *>(kp.out)[2 * k + lane] = lane ? make_uint2(c[2], c[3])
+                                                                      : make_uint2(c[0], c[1]);
+        } else {
+            uint32_t r[10];
+            pack_record(pk, rss_hash, rss_queue, r);
+            if (lane < 5) {
+                uint32_t xx = r[0], yy = r[1];
 #pragma unroll
-            for (int i = 1; i < 5; ++i)
-                if (lane == (uint32_t)i) xx = r[2 * i], yy = r[2 * i + 1];
-            reinterpret_cast<uint2 *>(kp.out + k)[lane] = make_uint2(xx, yy);
+                for (int i = 1; i < 5; ++i)
+                    if (lane == (uint32_t)i) xx = r[2 * i], yy = r[2 * i + 1];
+                reinterpret_cast<uint2 *>(kp.out + k)[lane] = make_uint2(xx, yy);
+            }
         }
-        if (kp.bins && lane == 0) kp.bins[k] = flow_bin(r[0], r[1], r[2], r[9] & 0xFFu);
+        if (kp.bins && lane == 0) kp.bins[k] = flow_bin(pk.saddr, pk.daddr, pk.ports, pk.verdict);
     }
 }
 
@@ -442,12 +451,8 @@ __global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
                 rss_queue = rss_core(rss_hash, kp.rss_nq, kp.rss_endian);
             }
         }
-        uint32_t r[10];
-        pack_record(pk, rss_hash, rss_queue, r);
-        uint2 *o = reinterpret_cast<uint2 *>(kp.out + kk);
-#pragma unroll
-        for (int i = 0; i < 5; ++i) o[i] = make_uint2(r[2 * i], r[2 * i + 1]);
-        if (kp.bins) kp.bins[kk] = flow_bin(r[0], r[1], r[2], r[9] & 0xFFu);
+        store_record(kp, kk, pk, rss_hash, rss_queue);
+        if (kp.bins) kp.bins[kk] = flow_bin(pk.saddr, pk.daddr, pk.ports, pk.verdict);
     }
 }
 

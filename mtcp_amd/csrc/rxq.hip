@@ -14,6 +14,7 @@
 // a wait does not wait for a later aggregate queued behind it.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stddef.h>
 #include <string.h>
 
 #include <new>
@@ -34,9 +35,10 @@ struct mtcp_gpu_rxq {
     hipEvent_t evt = nullptr;            // recorded after a flush's D2H
     uint8_t *buf = nullptr;              // pinned staging: frames, then room for descriptors
     mtcp_gpu_desc *desc = nullptr;       // pinned
-    mtcp_gpu_result *res = nullptr;      // pinned
+    uint8_t *res = nullptr;              // pinned result records (rec bytes each)
     uint8_t *d_buf = nullptr;            // device copy of buf
-    mtcp_gpu_result *d_out = nullptr;
+    uint8_t *d_out = nullptr;
+    uint32_t rec = 40;                   // record bytes: 40, or 16 for a compact context
     uint32_t max_pkts = 0;
     uint64_t max_bytes = 0;
     uint32_t n = 0;                      // frames staged
@@ -99,6 +101,7 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     q->max_pkts = max_pkts;
     q->max_bytes = (max_bytes + 63) & ~63ull;
     q->stream = reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx));
+    q->rec = mtcp_gpu_record_size(ctx);
     if (const char *e = getenv("MTCP_GPU_STAGE")) q->plain = strcmp(e, "plain") == 0;
     if (const char *e = getenv("MTCP_GPU_SERVE_AHEAD")) q->ahead = (uint32_t)atoi(e);
     if (const char *e = getenv("MTCP_GPU_SERVE_HINT")) q->hint = (uint32_t)atoi(e);
@@ -107,10 +110,9 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
         hipHostMalloc(&q->buf, staging, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&q->desc, (size_t)max_pkts * sizeof(mtcp_gpu_desc), hipHostMallocDefault) !=
             hipSuccess ||
-        hipHostMalloc(&q->res, (size_t)max_pkts * sizeof(mtcp_gpu_result), hipHostMallocDefault) !=
-            hipSuccess ||
+        hipHostMalloc(&q->res, (size_t)max_pkts * q->rec, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&q->d_buf, staging) != hipSuccess ||
-        hipMalloc(&q->d_out, (size_t)max_pkts * sizeof(mtcp_gpu_result)) != hipSuccess) {
+        hipMalloc(&q->d_out, (size_t)max_pkts * q->rec) != hipSuccess) {
         mtcp_gpu_rxq_destroy(q);
         return MTCP_GPU_ENOMEM;
     }
@@ -120,7 +122,7 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     // (copies the size of a flush's: small ones take another path)
     int rc = mtcp_gpu_reserve(ctx, 0, 0);
     const uint64_t h2d = staging < (1ull << 20) ? staging : (1ull << 20);
-    const uint64_t d2h = (uint64_t)max_pkts * sizeof(mtcp_gpu_result);
+    const uint64_t d2h = (uint64_t)max_pkts * q->rec;
     memset(q->buf, 0, h2d);
     if (rc == MTCP_GPU_OK &&
         (hipMemcpyAsync(q->d_buf, q->buf, h2d, hipMemcpyHostToDevice, q->stream) != hipSuccess ||
@@ -199,9 +201,9 @@ int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
         return MTCP_GPU_EIO;
     int rc = mtcp_gpu_rx_chunk_dev(q->ctx, q->d_buf, q->used,
                                    reinterpret_cast<const mtcp_gpu_desc *>(q->d_buf + q->used), cnt,
-                                   6, q->d_out, q->stream);
+                                   6, reinterpret_cast<mtcp_gpu_result *>(q->d_out), q->stream);
     if (rc == MTCP_GPU_OK &&
-        (hipMemcpyAsync(q->res + first, q->d_out, (size_t)cnt * sizeof(mtcp_gpu_result),
+        (hipMemcpyAsync(q->res + (size_t)first * q->rec, q->d_out, (size_t)cnt * q->rec,
                         hipMemcpyDeviceToHost, q->stream) != hipSuccess ||
          hipEventRecord(q->evt, q->stream) != hipSuccess))
         rc = MTCP_GPU_EIO;
@@ -243,16 +245,19 @@ uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
     if (!q || i >= q->done_n) return nullptr;
     if (q->ahead && i + q->ahead < q->done_n) {
         serve_prefetch(q->buf + ((uint64_t)q->desc[i + q->ahead].offset << 6), q->hint);
-        serve_prefetch(&q->res[i + q->ahead], q->hint);
+        serve_prefetch(q->res + (size_t)(i + q->ahead) * q->rec, q->hint);
     }
-    const mtcp_gpu_result &r = q->res[i];
+    const uint8_t *r = q->res + (size_t)i * q->rec;
+    // the verdict byte: mtcp_gpu_result.verdict (36) or mtcp_gpu_result16.verdict (14)
+    const uint8_t verdict = r[q->rec == 16 ? offsetof(mtcp_gpu_result16, verdict)
+                                           : offsetof(mtcp_gpu_result, verdict)];
     if (len) *len = q->desc[i].len;
-    if (res) *res = &r;
+    if (res) *res = reinterpret_cast<const mtcp_gpu_result *>(r);
     // core.c:774-775 counts NULL as rx_errors: the checksum failures, and the
     // frames whose headers claim bytes past the frame (the reference would
     // read past len there; the GPU computed no checksum to vouch for them)
-    if (r.verdict == MTCP_GPU_V_IP_CSUM_BAD || r.verdict == MTCP_GPU_V_TCP_CSUM_BAD ||
-        r.verdict == MTCP_GPU_V_TRUNCATED)
+    if (verdict == MTCP_GPU_V_IP_CSUM_BAD || verdict == MTCP_GPU_V_TCP_CSUM_BAD ||
+        verdict == MTCP_GPU_V_TRUNCATED)
         return nullptr;
     return q->buf + ((uint64_t)q->desc[i].offset << 6);
 }

@@ -15,10 +15,11 @@ import ctypes
 import numpy as np
 
 from ._lib import check, lib
-from ._types import ADDR_ENTRY_DTYPE, DESC_DTYPE, MAX_PORT, MIN_PORT, RESULT_DTYPE
+from ._types import ADDR_ENTRY_DTYPE, DESC_DTYPE, MAX_PORT, MIN_PORT, RESULT16_DTYPE, RESULT_DTYPE
 
 F_RSS = 0x1
 F_RSS_ENDIAN = 0x2
+F_COMPACT = 0x4
 
 PKT_TX_IP_CSUM = 0x01
 PKT_TX_TCP_CSUM = 0x02
@@ -51,10 +52,11 @@ class Context:
     the work PyTorch has queued on its current stream, as a torch op would."""
 
     def __init__(self, device: int = 0, rss: bool = False, rss_key: bytes | None = None,
-                 rss_queues: int = 1, rss_endian: bool = True):
+                 rss_queues: int = 1, rss_endian: bool = True, compact: bool = False):
         L = lib()
         self._h = ctypes.c_void_p()
         flags = (F_RSS if rss else 0) | (F_RSS_ENDIAN if (rss and rss_endian) else 0)
+        flags |= F_COMPACT if compact else 0
         key = None
         if rss_key is not None:
             if len(rss_key) != 40:
@@ -64,6 +66,18 @@ class Context:
         check(L.mtcp_gpu_open(ctypes.byref(self._h), device, key, rss_queues, flags),
               "mtcp_gpu_open")
         self.device = device
+        self.compact = compact
+        # the rx records this context writes (numpy dtype of one record)
+        self.result_dtype = RESULT16_DTYPE if compact else RESULT_DTYPE
+
+    @property
+    def record_size(self) -> int:
+        return lib().mtcp_gpu_record_size(self._h)
+
+    @property
+    def last_kernel(self) -> str:
+        """The kernel the last rx / tx launch dispatched (mtcp_gpu_last_kernel)."""
+        return lib().mtcp_gpu_last_kernel(self._h).decode()
 
     # -- lifetime ----------------------------------------------------------
     def close(self) -> None:
@@ -158,7 +172,9 @@ class Context:
                  out: np.ndarray | None = None) -> np.ndarray:
         desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
         if out is None:
-            out = np.zeros(len(desc), dtype=RESULT_DTYPE)
+            out = np.zeros(len(desc), dtype=self.result_dtype)
+        if out.dtype.itemsize != self.result_dtype.itemsize:
+            raise ValueError("out must hold this context's records (compact: 16 B)")
         check(lib().mtcp_gpu_rx_chunk(self._h, buf.ctypes.data, buf.nbytes, desc.ctypes.data,
                                       len(desc), off_shift, out.ctypes.data), "mtcp_gpu_rx_chunk")
         return out
@@ -168,7 +184,7 @@ class Context:
         arrs = [np.ascontiguousarray(np.frombuffer(bytes(f), dtype=np.uint8)) for f in frames]
         ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
         lens = np.array([a.nbytes for a in arrs], dtype=np.uint16)
-        out = np.zeros(n, dtype=RESULT_DTYPE)
+        out = np.zeros(n, dtype=self.result_dtype)
         check(lib().mtcp_gpu_rx_ptrs(self._h, ctypes.cast(ptrs, ctypes.c_void_p),
                                      lens.ctypes.data, n, out.ctypes.data), "mtcp_gpu_rx_ptrs")
         return out

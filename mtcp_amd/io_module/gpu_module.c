@@ -58,6 +58,12 @@
  * a GPU round trip (gather, H2D, kernel, D2H) that costs more than the CPU's
  * own fill of 64 frames (measured: DESIGN.md §7).
  *
+ * Device: the thread's GPU context opens a device on its core's NUMA node,
+ * dealt round-robin among that node's devices (gpu_topo.h; mTCP binds each
+ * thread's memory to its core's node, mtcp/src/cpu.c:54-79, and DPDK puts
+ * each port's queues on the NIC's socket, dpdk_module.c:660-663);
+ * MTCP_GPU_DEVICE=d forces one.
+ *
  * Resources per mTCP thread: one GPU context (one HIP stream), and, for each
  * of the CONFIG.eths_num interfaces (mtcp.h:138), two rxqs (pinned staging
  * of GPU_AGG_BURSTS x GPU_BURST frames of up to GPU_FRAME_MAX bytes each,
@@ -76,6 +82,7 @@
 
 #include "mtcp_gpu.h"
 #include "mtcp_gpu_rxq.h"
+#include "gpu_topo.h"
 
 #define GPU_AGG_BURSTS 64                 /* bursts per GPU launch           */
 #define GPU_BURST      64                 /* PS_CHUNK_SIZE / MAX_PKT_BURST   */
@@ -207,12 +214,35 @@ static struct gpu_ifq *gpu_ifq_get(struct gpu_private_context *g, int ifidx)
     return f;
 }
 
+/* The device of the mTCP thread on `cpu`: one on the core's NUMA node
+ * (gpu_topo.h); MTCP_GPU_DEVICE=d in the environment forces device d. */
+static int gpu_pick_device(int cpu, int ndev)
+{
+    const char *forced = getenv("MTCP_GPU_DEVICE");
+    const char *sysfs = gpu_topo_sysfs();
+    int dev_node[GPU_TOPO_MAX_DEVS], d, rank = 0, node;
+
+    if (forced && *forced) {
+        d = atoi(forced);
+        return d >= 0 && d < ndev ? d : -1;
+    }
+    if (ndev > GPU_TOPO_MAX_DEVS)
+        ndev = GPU_TOPO_MAX_DEVS;
+    for (d = 0; d < ndev; d++) {
+        char bdf[64];
+        dev_node[d] = mtcp_gpu_device_pci_bus_id(d, bdf, (int)sizeof(bdf)) == MTCP_GPU_OK
+                          ? gpu_topo_pci_node(sysfs, bdf) : -1;
+    }
+    node = gpu_topo_cpu_node(sysfs, cpu, &rank);
+    return gpu_topo_pick(cpu, node, rank, ndev, dev_node);
+}
+
 static void gpu_init_handle(struct mtcp_thread_context *ctx)
 {
     struct gpu_private_context *g = calloc(1, sizeof(*g));
     const char *pl = getenv("MTCP_GPU_PIPELINE");
     const char *tx = getenv("MTCP_GPU_TX");
-    int ndev, i;
+    int ndev, dev, i;
 
     gpu_inner_module->init_handle(ctx);       /* sets ctx->io_private_context */
     if (!g) {
@@ -233,7 +263,9 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
     }
 
     ndev = mtcp_gpu_device_count();
-    if (ndev <= 0 || mtcp_gpu_open(&g->gpu, ctx->cpu % ndev, NULL, 1, 0) != MTCP_GPU_OK ||
+    dev = ndev > 0 ? gpu_pick_device(ctx->cpu, ndev) : -1;
+    /* compact 16 B records: the rxqs read the verdict only (40 -> 16 B of D2H per frame) */
+    if (dev < 0 || mtcp_gpu_open(&g->gpu, dev, NULL, 1, MTCP_GPU_F_COMPACT) != MTCP_GPU_OK ||
         mtcp_gpu_reserve(g->gpu, 0, 0) != MTCP_GPU_OK) {     /* load the kernels now */
         if (g->gpu)
             mtcp_gpu_close(g->gpu);

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == set(_lib.EXPORTS), decl ^ set(_lib.EXPORTS)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mtcp_gpu_abi_version() == 1
+    assert lib.mtcp_gpu_abi_version() == 2
     assert lib.mtcp_gpu_strerror(-22) == b"invalid argument"
 
 
@@ -47,6 +47,26 @@ def test_struct_layouts():
     assert RESULT_DTYPE.itemsize == 40
     assert RESULT_DTYPE.fields["verdict"][1] == 36
     assert RESULT_DTYPE.fields["eth_type"][1] == 38
+    from mtcp_amd import RESULT16_DTYPE
+    assert RESULT16_DTYPE.itemsize == 16       # mtcp_gpu_result16 (MTCP_GPU_F_COMPACT)
+    assert RESULT16_DTYPE.fields["verdict"][1] == 14
+    assert RESULT16_DTYPE.fields["rss_hash"][1] == 0
+    hdr = open(os.path.join(ROOT, "include", "mtcp_gpu.h")).read()
+    assert re.search(r"uint8_t\s+verdict;\s+/\* 14 \*/", hdr)
+
+
+def test_compact_projection_keeps_same_named_fields():
+    import numpy as np
+    from mtcp_amd import RESULT16_DTYPE, RESULT_DTYPE, compact_of
+    r = np.zeros(3, RESULT_DTYPE)
+    r["verdict"] = [0, 9, 4]
+    r["tcp_csum"] = [0, 0x1234, 0]
+    r["rss_hash"] = [1, 2, 0xFFFFFFFF]
+    r["ihl_doff"] = [0x55, 0x85, 5]
+    c = compact_of(r)
+    assert c.dtype == RESULT16_DTYPE
+    for f in RESULT16_DTYPE.names:
+        assert np.array_equal(c[f], r[f]), f
 
 
 def test_no_gpu_no_fallback():
