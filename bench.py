@@ -138,6 +138,24 @@ def lib_sha256() -> str:
     return _codeobj.lib_sha256(_lib.LIB_PATH)
 
 
+def pmc_traffic(name: str):
+    """HBM bytes per launch of the dominant kernel from the committed
+    rocprofv3 PMC profile (profiles/traffic_<name>.json: FETCH_SIZE x 2 +
+    WRITE_SIZE, separate passes, tools/profile_config.sh), when it was taken
+    on this build or one with the same rx sources; else (None, why)."""
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"traffic_{name}.json")
+    if not os.path.exists(tpath):
+        return None, "no PMC profile for this config"
+    tj = json.load(open(tpath))
+    if tj.get("lib_sha256") == lib_sha256():
+        return tj.get("hbm_bytes_per_launch"), f"rocprofv3 PMC of this build ({os.path.relpath(tpath)})"
+    if tj.get("rx_source_key") == _codeobj.rx_source_key():
+        return tj.get("hbm_bytes_per_launch"), (f"rocprofv3 PMC of a build with the same rx sources "
+                                                f"({os.path.relpath(tpath)}; the library differs elsewhere)")
+    return None, (f"stale: {os.path.relpath(tpath)} was collected on another build "
+                  f"({tj.get('hbm_bytes_per_launch')} B per launch there)")
+
+
 def cpu_share() -> int:
     n = len(os.sched_getaffinity(0))
     return max(1, min(n, 16))   # the GPU box's CPU share per GPU is 16
@@ -321,12 +339,25 @@ def run_row(args):
         algo = frame_bytes + 4 * n
         line.update(value=round(frame_bytes / wall / 1e9, 2), unit="GB/s", dtype="u8",
                     ms_per_step=round(wall * 1e3, 5), gpkt_per_s=round(n / wall / 1e9, 4))
+        traffic, traffic_note = pmc_traffic("f1")
         line["roofline"] = {"bound": "hbm", "achieved": round(algo / kern / 1e9, 2),
                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                            "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                            "traffic_source": traffic_note,
+                            "kernel": "mg::" + ctx.last_kernel,
                             "avg_launch_ms": round(kern * 1e3, 5),
                             "algorithmic_bytes_per_launch": algo,
                             "note": "sum L read + 4 B of check fields written per frame"}
+        # the access pattern's own ceiling: one 2 x 2-byte patch per 1536 B
+        # slot costs a 32 B write granule and a dirty sector per frame
+        # (DESIGN §7), measured by tools/store_probe.hip slot_patch
+        cj = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "ceilings.json")
+        if os.path.exists(cj):
+            c = json.load(open(cj)).get("f1")
+            if c:
+                line["roofline"]["ceiling_us"] = c["us_per_launch"]
+                line["roofline"]["ceiling_frac"] = round(c["us_per_launch"] / (kern * 1e6), 4)
+                line["roofline"]["ceiling_source"] = c["source"]
         if want_cpu:
             import oracle   # test infrastructure: the baseline leg only
             host = d_buf.cpu().numpy()
@@ -609,30 +640,16 @@ def main():
         # per-GPU roofline of the slowest rank's launches (N > 1: the max
         # over ranks of the event-timed average launch)
         achieved = frame_bytes / (kern_ms_max / 1e3) / 1e9
-        traffic, traffic_note = None, "no PMC profile for this config"
-        tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                             # C4's per-GPU step is two launches of C2's shape (1 M x 1500 B
-                             # each): the per-launch figure is C2's
-                             f"traffic_{'c2' if args.config == 'c4' else args.config}"
-                             f"{'_compact' if compact else ''}.json")
-        if os.path.exists(tpath):
-            tj = json.load(open(tpath))
-            if tj.get("lib_sha256") == lib_sha256():
-                traffic = tj.get("hbm_bytes_per_launch")
-                traffic_note = f"rocprofv3 PMC of this build ({os.path.relpath(tpath)})"
-            elif tj.get("rx_source_key") == _codeobj.rx_source_key():
-                traffic = tj.get("hbm_bytes_per_launch")
-                traffic_note = (f"rocprofv3 PMC of a build with the same rx_kernel sources "
-                                f"({os.path.relpath(tpath)}; the library differs elsewhere)")
-            else:
-                traffic_note = (f"stale: {os.path.relpath(tpath)} was collected on another build "
-                                f"({tj.get('hbm_bytes_per_launch')} B per launch there)")
-            if traffic is not None and args.config == "c4":
-                # a C4 step (the unit of avg_launch_ms and of the algorithmic
-                # bytes here) is two launches of C2's shape: C2's per-launch
-                # traffic scaled by the frame bytes
-                traffic = round(traffic * frame_bytes / CONFIGS["c2"]["per_gpu"] / 1500)
-                traffic_note += "; C2's per-launch figure x the C4 step's frame bytes / C2's"
+        # C4's per-GPU step is two launches of C2's shape (1 M x 1500 B each):
+        # the per-launch figure is C2's
+        traffic, traffic_note = pmc_traffic(f"{'c2' if args.config == 'c4' else args.config}"
+                                            f"{'_compact' if compact else ''}")
+        if traffic is not None and args.config == "c4":
+            # a C4 step (the unit of avg_launch_ms and of the algorithmic
+            # bytes here) is two launches of C2's shape: C2's per-launch
+            # traffic scaled by the frame bytes
+            traffic = round(traffic * frame_bytes / CONFIGS["c2"]["per_gpu"] / 1500)
+            traffic_note += "; C2's per-launch figure x the C4 step's frame bytes / C2's"
         line = {
             "metric": METRIC, "value": round(gbs, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),

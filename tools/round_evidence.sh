@@ -3,20 +3,27 @@
 # time limit (tools/gpu_steps.sh stops at the first fault or timeout):
 #   /usr/local/graft/bin/gpurun --timeout 1150 -- 'bash tools/round_evidence.sh'
 # then, back in the build container:
-#   python3 tools/update_profiles.py rNN c2 c3 c5   (+ copy the row / probe outputs)
+#   python3 tools/update_profiles.py rNN c2 c3 c3_compact c5 f1   (+ copy the row / probe outputs)
+# Order: the PMC passes first, then `update_profiles.py --traffic` writes
+# profiles/traffic_<cfg>.json for THIS build, then the bench lines, so every
+# committed bench line quotes the traffic of the library it measured.
 bash tools/gpu_steps.sh \
   "pyt|300|python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread" \
   "smoke|100|python -c \"import __graft_entry__ as g; g.smoke()\"" \
-  "b1|150|python bench.py --config c1" \
-  "b2|150|python bench.py --config c2" \
-  "b3|150|python bench.py --config c3" \
-  "b4|150|python bench.py --config c4" \
-  "b5|200|python bench.py --config c5" \
   "p2|200|bash tools/profile_config.sh c2 gpurun_out/prof_c2" \
   "p3|200|bash tools/profile_config.sh c3 gpurun_out/prof_c3" \
+  "p3c|200|bash tools/profile_config.sh c3_compact gpurun_out/prof_c3_compact" \
   "p5|240|bash tools/profile_config.sh c5 gpurun_out/prof_c5" \
-  "f1|150|python bench.py --config f1" \
-  "f3|150|python bench.py --config f3" \
-  "f4|150|python bench.py --config f4" \
+  "pf1|200|bash tools/profile_config.sh f1 gpurun_out/prof_f1" \
+  "tr|60|python3 tools/update_profiles.py --traffic c2 c3 c3_compact c5 f1" \
+  "bc1|150|python bench.py --config c1" \
+  "bc2|150|python bench.py --config c2" \
+  "bc3|150|python bench.py --config c3" \
+  "bc3_compact|150|python bench.py --config c3 --record compact" \
+  "bc4|150|python bench.py --config c4" \
+  "bc5|200|python bench.py --config c5" \
+  "bf1|150|python bench.py --config f1" \
+  "bf3|150|python bench.py --config f3" \
+  "bf4|150|python bench.py --config f4" \
   "pr|240|bash tools/profile_rows.sh gpurun_out/prof_rows" \
   "wp|120|./tools/wave_probe 1500 64 1024 4096 16384 32768 && ./tools/wave_probe 9000 64 4096 16384 && ./tools/wave_probe 64 64 4096 16384 65536"

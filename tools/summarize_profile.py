@@ -11,7 +11,9 @@ import statistics
 import sys
 
 src, cfg, out = sys.argv[1], sys.argv[2], sys.argv[3]
-algo = {"c2": 1572864000, "c3": 819090368, "c5": 4718592000}[cfg]
+# algorithmic bytes per launch: sum L (rx), sum L + 4 B of check fields per frame (f1)
+algo = {"c2": 1572864000, "c3": 819090368, "c3_compact": 819090368, "c5": 4718592000,
+        "f1": 1572864000 + 4 * (1 << 20)}[cfg]
 
 
 def rows(pattern):
