@@ -4,3 +4,4 @@ for r in 1 2 3; do
 timeout -k 10 120 python bench.py --config c3 --steps 200 --warmup 20 --cpu-baseline off --pcie off --small-batch off >> gpurun_out/r3_c3_ab.jsonl
 timeout -k 10 120 python bench.py --config c3 --record compact --steps 200 --warmup 20 --cpu-baseline off --pcie off --small-batch off >> gpurun_out/r3_c3_ab.jsonl
 done
+timeout -k 10 400 bash tools/small_batch_trace.sh gpurun_out/sbt_graph graph
