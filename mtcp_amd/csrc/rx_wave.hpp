@@ -1,5 +1,5 @@
 // rx_wave.hpp — one wavefront per packet: the shape BASELINE.json's north
-// star names, dispatched for small batches (mtcp_gpu.hip kWaveUpToPkts).
+// star names, dispatched for small batches (mtcp_gpu.hip pick_sched).
 //
 // rx_kernel (rx_kernels.hpp) gives a wave 64 packets and streams them four
 // at a time through 16-lane rows; on 1 M-packet batches that keeps every
@@ -78,12 +78,13 @@ __device__ __forceinline__ uint32_t toeplitz_wave(const uint32_t (&kw)[4], uint3
 // NL: 16 B loads per lane per trip (a trip covers 1 KiB * NL of frame):
 // 2 for MTU-sized batches, kWaveLoads for jumbo ones (mtcp_gpu.hip picks by
 // the batch's average slot); fewer unrolled loads, fewer instructions.
-template <int MODE, bool RSS, int ABL = 0, int SEG = 1, int NL = kWaveLoads>
-__global__ __launch_bounds__(kBlock) void rx_wave_kernel(KParams kp) {
-    __shared__ uint4 lds[kWavesPerBlock][kSlotChunks];     // the frame's chunks 0..6
+// WPB: waves (= packets) per workgroup.
+template <int MODE, bool RSS, int ABL = 0, int SEG = 1, int NL = kWaveLoads, int WPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWave * WPB) void rx_wave_kernel(KParams kp) {
+    __shared__ uint4 lds[WPB][kSlotChunks];                // the frame's chunks 0..6
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t k = blockIdx.x * kWavesPerBlock + wib;  // this wave's packet
+    const uint32_t k = blockIdx.x * WPB + wib;             // this wave's packet
     if (k >= kp.n) return;
     uint4 *hd4 = lds[wib];
     const uint32_t *hd = reinterpret_cast<const uint32_t *>(hd4);

@@ -21,8 +21,9 @@
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
-__global__ __launch_bounds__(256) void empty_kernel(mg::KParams kp) {
-    const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void empty_kernel(mg::KParams kp) {
+    const uint32_t k = blockIdx.x * WPB + (threadIdx.x >> 6);
     if (k < kp.n && (threadIdx.x & 63) == 0) kp.out[k].saddr = k;
 }
 
@@ -41,7 +42,10 @@ int main(int argc, char **argv) {
     // threads per block and packets per block of each variant
     struct V { const char *name; kfn fn; uint32_t threads, ppb; };
     const V vs[] = {
-        {"empty", empty_kernel, 256, 4},
+        {"empty", empty_kernel<4>, 256, 4},
+        {"empty16", empty_kernel<16>, 1024, 16},
+        {"w8nl2", mg::rx_wave_kernel<mg::kRxChunk, false, 0, 1, 2, 8>, 512, 8},
+        {"w16nl2", mg::rx_wave_kernel<mg::kRxChunk, false, 0, 1, 2, 16>, 1024, 16},
         {"desc", mg::rx_wave_kernel<mg::kRxChunk, false, 2>, 256, 4},
         {"phase1", mg::rx_wave_kernel<mg::kRxChunk, false, 1>, 256, 4},
         {"full", mg::rx_wave_kernel<mg::kRxChunk, false, 0>, 256, 4},
@@ -106,7 +110,7 @@ int main(int argc, char **argv) {
             printf(", \"%s_us\": %.2f", v.name, t[t.size() / 2]);
             // every full variant's records must equal the wave kernel's
             static std::vector<mtcp_gpu_result> ref;
-            const bool full = !strchr(v.name, '_') && strcmp(v.name, "empty") && strcmp(v.name, "desc") &&
+            const bool full = !strchr(v.name, '_') && strncmp(v.name, "empty", 5) && strcmp(v.name, "desc") &&
                               strcmp(v.name, "phase1") && strcmp(v.name, "head") && strcmp(v.name, "segsum") &&
                               strcmp(v.name, "p1nl2");
             if (full) {
