@@ -55,3 +55,6 @@ tests/c/rxloop: tests/c/rxloop.c mtcp_amd/io_module/gpu_module.c include/mtcp_gp
 
 tools/wave_probe: tools/wave_probe.hip mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/rx_kernels.hpp $(LIB)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
+
+tools/occ_probe: tools/occ_probe.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'

@@ -706,10 +706,12 @@ struct Trip {
 // CMP: write 16 B mtcp_gpu_result16 records (MTCP_GPU_F_COMPACT) — four dwords
 // held per pass instead of ten, plus the flow bin when one is asked for (the
 // compact record has no 4-tuple to hash at the flush).
+// WPE: waves per SIMD the register allocation must allow (2: up to 256
+// VGPRs; 3: 168, a third workgroup per CU; tools/occ_probe.hip).
 template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
           bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0,
-          int WPB = kWavesPerBlock, int XSKIP = 0, bool CMP = false>
-__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(2))) void rx_kernel(KParams kp) {
+          int WPB = kWavesPerBlock, int XSKIP = 0, bool CMP = false, int WPE = 2>
+__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE))) void rx_kernel(KParams kp) {
     uint64_t t_start = 0;
     if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
     if constexpr ((PRIO & 3) > 0) {
