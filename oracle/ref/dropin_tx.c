@@ -1,0 +1,261 @@
+/*
+ * dropin_tx.c — TEST HARNESS (oracle/_ref build: needs /root/reference to
+ * build; the binary then runs on the GPU box like the other oracle/_ref
+ * files).
+ *
+ * The tx drop-in at the reference's REAL call sites: mTCP's
+ * own transmit builders — SendTCPPacketStandalone (mtcp/src/tcp_out.c:135-218)
+ * -> IPOutputStandalone (ip_out.c:35-98) -> GetOutputInterface (ip_out.c:8-33),
+ * GetDestinationHWaddr (arp.c:93-119) -> EthernetOutput (eth_out.c:35-80) ->
+ * mtcp->iom->get_wptr — compiled from /root/reference WITHOUT
+ * -DDISABLE_HWCSUM, so that ip_out.c:76-91 asks
+ * dev_ioctl(PKT_TX_TCPIP_CSUM_PEEK) (PKT_TX_IP_CSUM for ICMP) and
+ * tcp_out.c:201-211 dev_ioctl(PKT_TX_TCPIP_CSUM), and computes ip_fast_csum /
+ * TCPCalcChecksum only on -1.  mtcp->iom is gpu_module_func
+ * (mtcp_amd/io_module/gpu_module.c, mTCP's real headers), wrapping a NIC-like
+ * backend whose get_wptr hands out the slots of one tx buffer and whose
+ * send_pkts "transmits" them (copies them to the output, reuses the buffer);
+ * mtcp->iom->send_pkts runs every 64 frames as RunMainLoop's tx section does
+ * (core.c:818-824, MAX_PKT_BURST).
+ *
+ * With MTCP_GPU_TX=1 and a GPU, dev_ioctl answers 0, mTCP leaves both check
+ * fields 0, and gpu_module fills them on the GPU at send_pkts; with
+ * MTCP_GPU_TX=0 (or no GPU) it answers -1 and mTCP fills them itself: the same
+ * binary produces the reference's own frames.  tests/test_dropin.py compares
+ * the two byte for byte.
+ *
+ * Observation only: `--wrap=TCPCalcChecksum` counts the reference's software
+ * TCP checksums; mode "observe" logs dev_ioctl's answers through a copy of
+ * gpu_module_func (mode "plain": mtcp->iom = &gpu_module_func).  The routing
+ * and ARP tables are mTCP's own (CONFIG.rtable, CONFIG.arp) with one entry
+ * each; the symbols tcp_out.c names for the stateful sender (not reached
+ * from the standalone builder) are aborting stubs (ref/tx_stubs.c).
+ *
+ *   dropin_tx OUT N [observe|plain]
+ *     OUT  N records of 2048 B: u16 len, u16 proto, 4 B pad, then the frame
+ *          as the NIC sent it
+ *   prints one JSON line
+ */
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mtcp.h"
+#include "io_module.h"
+#include "ip_out.h"
+#include "tcp_in.h"
+#include "tcp_out.h"
+
+struct mtcp_config CONFIG;
+extern io_module_func gpu_module_func;
+extern io_module_func *gpu_inner_module;
+
+#define SLOT 2048
+#define BURST 64
+
+/* ---- observation points ------------------------------------------------- */
+static uint64_t g_tcp_csum_calls;
+uint16_t __real_TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t daddr);
+uint16_t __wrap_TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t daddr)
+{
+    g_tcp_csum_calls++;
+    return __real_TCPCalcChecksum(buf, len, saddr, daddr);
+}
+
+static int g_ioctl_peek = -2, g_ioctl_tcpip = -2, g_ioctl_ip = -2;
+static io_module_func g_observed;
+static int32_t observe_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp)
+{
+    int32_t r = gpu_module_func.dev_ioctl(ctx, nif, cmd, argp);
+    if (cmd == PKT_TX_TCPIP_CSUM_PEEK) g_ioctl_peek = r;
+    if (cmd == PKT_TX_TCPIP_CSUM) g_ioctl_tcpip = r;
+    if (cmd == PKT_TX_IP_CSUM) g_ioctl_ip = r;
+    return r;
+}
+
+/* ---- the wrapped backend: one tx buffer of BURST slots -------------------- */
+struct fake_nic {
+    uint8_t buf[BURST][SLOT];
+    uint16_t len[BURST];
+    uint32_t queued;
+    uint8_t *out;          /* the sent frames, in send order */
+    uint32_t sent, cap;
+    int send_calls, full;
+};
+static struct fake_nic *g_nic;
+
+static void nic_load(void) {}
+static void nic_init(struct mtcp_thread_context *ctx) { ctx->io_private_context = g_nic; }
+static int32_t nic_link(struct mtcp_thread_context *ctx) { (void)ctx; return 0; }
+static void nic_release(struct mtcp_thread_context *ctx, int ifidx, unsigned char *p, int len)
+{
+    (void)ctx; (void)ifidx; (void)p; (void)len;
+}
+static uint8_t *nic_wptr(struct mtcp_thread_context *ctx, int ifidx, uint16_t len)
+{
+    struct fake_nic *f = ctx->io_private_context;
+    (void)ifidx;
+    if (f != g_nic) { fprintf(stderr, "context swap broken\n"); exit(3); }
+    if (f->queued == BURST || len > SLOT) {
+        f->full++;
+        return NULL;                         /* mTCP retries after send_pkts */
+    }
+    f->len[f->queued] = len;
+    memset(f->buf[f->queued], 0xA5, SLOT);   /* whatever the slot held before */
+    return f->buf[f->queued++];
+}
+static int32_t nic_send(struct mtcp_thread_context *ctx, int nif)
+{
+    struct fake_nic *f = ctx->io_private_context;
+    uint32_t i;
+    (void)nif;
+    if (f != g_nic) { fprintf(stderr, "context swap broken\n"); exit(3); }
+    f->send_calls++;
+    for (i = 0; i < f->queued && f->sent < f->cap; i++, f->sent++) {
+        uint8_t *rec = f->out + (size_t)f->sent * SLOT;
+        uint16_t proto = f->buf[i][23];
+        memcpy(rec, &f->len[i], 2);
+        memcpy(rec + 2, &proto, 2);
+        memcpy(rec + 8, f->buf[i], f->len[i] < SLOT - 8 ? f->len[i] : SLOT - 8);
+    }
+    f->queued = 0;                           /* the NIC reuses its buffer */
+    return 0;
+}
+static uint8_t *nic_rptr(struct mtcp_thread_context *ctx, int ifidx, int index, uint16_t *len)
+{
+    (void)ctx; (void)ifidx; (void)index;
+    *len = 0;
+    return NULL;
+}
+static int32_t nic_recv(struct mtcp_thread_context *ctx, int ifidx) { (void)ctx; (void)ifidx; return 0; }
+static int32_t nic_select(struct mtcp_thread_context *ctx) { (void)ctx; return 0; }
+static void nic_destroy(struct mtcp_thread_context *ctx) { ctx->io_private_context = NULL; }
+
+static io_module_func nic_module = {
+    .load_module = nic_load, .init_handle = nic_init, .link_devices = nic_link,
+    .release_pkt = nic_release, .get_wptr = nic_wptr, .send_pkts = nic_send,
+    .get_rptr = nic_rptr, .recv_pkts = nic_recv, .select = nic_select,
+    .destroy_handle = nic_destroy, .dev_ioctl = NULL,
+};
+
+static uint64_t g_rng = 0x2545F4914F6CDD1Dull;
+static uint64_t rnd(void)
+{
+    uint64_t z = (g_rng += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+int main(int argc, char **argv)
+{
+    static const uint8_t flag_set[8] = {
+        TCP_FLAG_ACK, TCP_FLAG_ACK | TCP_FLAG_PSH, TCP_FLAG_SYN, TCP_FLAG_SYN | TCP_FLAG_ACK,
+        TCP_FLAG_FIN | TCP_FLAG_ACK, TCP_FLAG_RST | TCP_FLAG_ACK, TCP_FLAG_RST,
+        TCP_FLAG_FIN | TCP_FLAG_PSH | TCP_FLAG_ACK};
+    static struct eth_table eths[1];
+    static struct route_table rt[1];
+    static struct arp_entry arp[1];
+    static int nif_to_eidx[1];
+    struct mtcp_thread_context ctx;
+    mtcp_manager_t mtcp;
+    uint8_t payload[TCP_DEFAULT_MSS + 64];
+    uint32_t n, i, tcp_frames = 0, icmp_frames = 0, refused = 0;
+    int observe;
+    FILE *out;
+
+    if (argc < 3) {
+        fprintf(stderr, "usage: dropin_tx OUT N [observe|plain]\n");
+        return 1;
+    }
+    n = (uint32_t)atoi(argv[2]);
+    observe = !(argc > 3 && strcmp(argv[3], "plain") == 0);
+
+    /* mtcp.conf's one port, one route, one ARP entry (config.c fills these) */
+    memcpy(eths[0].haddr, "\x02\x00\x00\x00\x00\x01", 6);
+    eths[0].ip_addr = 0x0100000A;
+    rt[0].mask = 0;
+    rt[0].masked = 0;
+    rt[0].prefix = 1;
+    rt[0].nif = 0;
+    arp[0].prefix = 8;
+    arp[0].ip_mask = 0;
+    arp[0].ip_masked = 0;
+    memcpy(arp[0].haddr, "\x02\x00\x00\x00\x00\x02", 6);
+    nif_to_eidx[0] = 0;
+    CONFIG.eths = eths;
+    CONFIG.eths_num = 1;
+    CONFIG.nif_to_eidx = nif_to_eidx;
+    CONFIG.rtable = rt;
+    CONFIG.routes = 1;
+    CONFIG.arp.entry = arp;
+    CONFIG.arp.entries = 1;
+
+    g_nic = calloc(1, sizeof(*g_nic));
+    g_nic->cap = n;
+    g_nic->out = calloc((size_t)n + 1, SLOT);
+    memset(&ctx, 0, sizeof(ctx));
+    mtcp = calloc(1, sizeof(*mtcp));
+    ctx.cpu = 0;
+    ctx.mtcp_manager = mtcp;
+    mtcp->ctx = &ctx;
+    if (observe) {
+        g_observed = gpu_module_func;
+        g_observed.dev_ioctl = observe_ioctl;
+        mtcp->iom = &g_observed;
+    } else {
+        mtcp->iom = &gpu_module_func;
+    }
+    gpu_inner_module = &nic_module;
+    mtcp->iom->load_module();
+    mtcp->iom->init_handle(&ctx);
+    mtcp->iom->link_devices(&ctx);
+
+    for (i = 0; i < n; i++) {
+        uint32_t saddr = (uint32_t)rnd(), daddr = (uint32_t)rnd();
+        uint16_t sport = (uint16_t)rnd(), dport = (uint16_t)rnd();
+        uint32_t k, len;
+        if (i % 97 == 96) {
+            /* an ICMP datagram: IP checksum per PKT_TX_IP_CSUM (ip_out.c:86-88) */
+            uint8_t *p = IPOutputStandalone(mtcp, IPPROTO_ICMP, (uint16_t)i, saddr, daddr, 64);
+            if (!p) { refused++; mtcp->iom->send_pkts(&ctx, 0); continue; }
+            for (k = 0; k < 64; k++) p[k] = (uint8_t)rnd();
+            icmp_frames++;
+        } else {
+            const uint8_t flags = flag_set[rnd() % 8];
+            const uint64_t r = rnd();
+            /* payload lengths: every length up to 64 for the first frames,
+             * then random up to the MSS (odd and even) */
+            len = i < 65 ? i : (uint32_t)(r % (TCP_DEFAULT_MSS + 1));
+            if (flags & (TCP_FLAG_SYN | TCP_FLAG_RST)) len = len % 17;
+            for (k = 0; k < len; k++) payload[k] = (uint8_t)rnd();
+            if (SendTCPPacketStandalone(mtcp, saddr, sport, daddr, dport, (uint32_t)rnd(),
+                                        (uint32_t)rnd(), (uint16_t)rnd(), flags, payload,
+                                        (uint16_t)len, (uint32_t)rnd(), (uint32_t)rnd()) < 0) {
+                refused++;
+                mtcp->iom->send_pkts(&ctx, 0);
+                continue;
+            }
+            tcp_frames++;
+        }
+        if ((i + 1) % BURST == 0)
+            mtcp->iom->send_pkts(&ctx, 0);               /* core.c:818-824 */
+    }
+    mtcp->iom->send_pkts(&ctx, 0);
+    mtcp->iom->destroy_handle(&ctx);
+
+    out = fopen(argv[1], "wb");
+    if (!out || fwrite(g_nic->out, SLOT, g_nic->sent, out) != g_nic->sent) { perror(argv[1]); return 1; }
+    fclose(out);
+    printf("{\"frames\": %u, \"sent\": %u, \"tcp\": %u, \"icmp\": %u, \"refused\": %u, "
+           "\"send_calls\": %d, \"tcp_csum_calls\": %llu, \"ioctl_peek\": %d, \"ioctl_tcpip\": %d, "
+           "\"ioctl_ip\": %d, \"observe\": %d}\n",
+           n, g_nic->sent, tcp_frames, icmp_frames, refused, g_nic->send_calls,
+           (unsigned long long)g_tcp_csum_calls, g_ioctl_peek, g_ioctl_tcpip, g_ioctl_ip, observe);
+    free(g_nic->out);
+    free(g_nic);
+    free(mtcp);
+    return 0;
+}

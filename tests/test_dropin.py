@@ -18,6 +18,13 @@ expectation is the --disable-hwcsum reference's own outcome for every frame
   frames).
 * no GPU (this container): dev_ioctl answers -1 and the reference computes
   everything itself: every branch as with --disable-hwcsum.
+
+The tx side (oracle/ref/dropin_tx.c): mTCP's own SendTCPPacketStandalone /
+IPOutputStandalone / EthernetOutput (tcp_out.c, ip_out.c, eth_out.c, arp.c
+WITHOUT -DDISABLE_HWCSUM) build frames into gpu_module's get_wptr buffers;
+with MTCP_GPU_TX=1 dev_ioctl answers 0, mTCP leaves the checks, the GPU fills
+them at send_pkts, and the frames sent equal those of the same reference
+code filling them itself (MTCP_GPU_TX=0).
 """
 import json
 import os
@@ -132,3 +139,71 @@ def test_dropin_at_the_reference_call_sites(tmp_path, golden, mode, pipeline):
     padded = ok & (br == BR_TCP_OK) & (14 + tot < ln)
     assert past.sum() >= 8 and (r["branch"][past] == NULL).all()
     assert padded.sum() >= 30 and (r["branch"][padded] == BR_TCP_OK).all()
+
+
+# ---- the tx side: SendTCPPacketStandalone / IPOutputStandalone ----------------
+EXE_TX = os.path.join(ROOT, "oracle", "_ref", "dropin_tx")
+TX_SLOT = 2048
+
+
+def run_dropin_tx(tmp_path, n=4096, tx="1", mode="observe"):
+    if not os.path.exists(EXE_TX):
+        pytest.fail("oracle/_ref/dropin_tx not built: `make -C oracle ref` (needs /root/reference)")
+    out = tmp_path / f"tx_{tx}_{mode}.bin"
+    p = subprocess.run([EXE_TX, str(out), str(n), mode], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MTCP_GPU_TX=tx, MTCP_GPU_PIPELINE="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    stats = json.loads(p.stdout.strip().splitlines()[-1])
+    recs = np.fromfile(out, dtype=np.uint8).reshape(-1, TX_SLOT)
+    return stats, recs
+
+
+def tx_frames_verify(recs):
+    """The sent frames through the oracle's rx chain: every TCP frame's IP and
+    TCP checksums verify (TCP_OK), every ICMP frame's IP checksum (ICMP)."""
+    import oracle
+    from mtcp_amd import DESC_DTYPE
+    lens = recs[:, 0:2].copy().view(np.uint16).ravel()
+    desc = np.zeros(len(recs), DESC_DTYPE)
+    desc["offset"] = np.arange(len(recs), dtype=np.uint32) * TX_SLOT + 8
+    desc["len"] = lens
+    v = oracle.rx_chunk(np.ascontiguousarray(recs).ravel(), desc, 0)["verdict"]
+    proto = recs[:, 8 + 23]
+    return v, proto
+
+
+def test_dropin_tx_passthrough_without_gpu(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    if not os.path.exists(EXE_TX):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    stats, recs = run_dropin_tx(tmp_path, tx="1")
+    assert stats["sent"] == stats["frames"] == len(recs) and stats["refused"] == 0
+    # no GPU: mTCP's own fills (ip_out.c:89-90, tcp_out.c:207-210)
+    assert stats["ioctl_peek"] == stats["ioctl_tcpip"] == stats["ioctl_ip"] == -1
+    assert stats["tcp_csum_calls"] == stats["tcp"] > 4000
+    v, proto = tx_frames_verify(recs)
+    assert (v[proto == 6] == 0).all() and (v[proto == 1] == 6).all() and stats["icmp"] > 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["observe", "plain"])
+def test_dropin_tx_at_the_reference_call_sites(tmp_path, mode):
+    """MTCP_GPU_TX=1: ip_out.c:76-84 gets 0 from dev_ioctl(PKT_TX_TCPIP_CSUM_PEEK)
+    and tcp_out.c:201-205 from dev_ioctl(PKT_TX_TCPIP_CSUM), so mTCP computes
+    neither checksum; gpu_module fills both on the GPU at send_pkts, and the
+    frames the NIC sends equal, byte for byte, the frames the same reference
+    code sends when it fills them itself (MTCP_GPU_TX=0: dev_ioctl -1).
+    ICMP (PKT_TX_IP_CSUM) stays with mTCP in both runs."""
+    stats, recs = run_dropin_tx(tmp_path, tx="1", mode=mode)
+    sw_stats, sw = run_dropin_tx(tmp_path, tx="0", mode=mode)
+    assert stats["sent"] == stats["frames"] == sw_stats["sent"] == len(recs) and stats["refused"] == 0
+    assert stats["tcp_csum_calls"] == 0 and sw_stats["tcp_csum_calls"] == sw_stats["tcp"] > 4000
+    if mode == "observe":
+        assert stats["ioctl_peek"] == 0 and stats["ioctl_tcpip"] == 0 and stats["ioctl_ip"] == -1
+        assert sw_stats["ioctl_peek"] == -1 and sw_stats["ioctl_tcpip"] == -1
+    assert stats["send_calls"] >= len(recs) // 64
+    assert np.array_equal(recs, sw)
+    v, proto = tx_frames_verify(recs)
+    assert (v[proto == 6] == 0).all() and (v[proto == 1] == 6).all()
