@@ -39,10 +39,10 @@
  * of that interface is healthy and -1 otherwise, so mTCP falls back to its
  * own checksums exactly as with a NIC that lacks the offload
  * (dpdk_dev_ioctl, dpdk_module.c:809-816).
- * NETSTAT difference: a frame dropped here never reaches ProcessPacket, so
- * it counts in rx_errors only, while the --disable-hwcsum path also counts
- * it in rx_packets / rx_bytes (eth_in.c:20-23) — as for dpdk_get_rptr's
- * NIC-verified drops.
+ * NETSTAT: a frame dropped here never reaches ProcessPacket, so get_rptr
+ * counts it in rx_packets / rx_bytes as ProcessPacket would have
+ * (eth_in.c:20-23) and core.c:774-775 counts the NULL in rx_errors: the three
+ * counters equal the --disable-hwcsum path's (tests/test_dropin.py).
  *
  * Transmit, with MTCP_GPU_TX=1 in the environment (psio or dpdk underneath;
  * refused over netmap, whose get_wptr sends the previous frame): dev_ioctl
@@ -471,15 +471,28 @@ static uint8_t *gpu_get_rptr(struct mtcp_thread_context *ctx, int ifidx, int ind
 {
     struct gpu_private_context *g = ctx->io_private_context;
     struct gpu_ifq *f = g->passthrough ? NULL : g->ifq[ifidx];
+    uint8_t *p;
     int a;
     if (!f)
         return INNER_CALL(ctx, gpu_inner_module->get_rptr(ctx, ifidx, index, len));
     a = f->serving;
     if (a < 0 || f->dropped[a][index])
-        return NULL;
+        return NULL;                  /* the wrapped backend's own NULL */
     if (f->served_raw[a])
         return mtcp_gpu_rxq_frame(f->rxq[a], (uint32_t)index, len);
-    return mtcp_gpu_rxq_get(f->rxq[a], (uint32_t)index, len, NULL);
+    p = mtcp_gpu_rxq_get(f->rxq[a], (uint32_t)index, len, NULL);
+#ifdef NETSTAT
+    if (!p && ctx->mtcp_manager) {
+        /* a frame dropped on its GPU verdict never reaches ProcessPacket,
+         * which counts every frame it is handed, checksum drops included
+         * (eth_in.c:20-23): count it here, so that rx_packets / rx_bytes /
+         * rx_errors (core.c:774-775) equal the software path's */
+        struct mtcp_manager *m = ctx->mtcp_manager;
+        m->nstat.rx_packets[ifidx]++;
+        m->nstat.rx_bytes[ifidx] += *len + 24;
+    }
+#endif
+    return p;
 }
 
 static int32_t gpu_select(struct mtcp_thread_context *ctx)

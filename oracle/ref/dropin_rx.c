@@ -339,10 +339,11 @@ int main(int argc, char **argv)
     if (!out || fwrite(recs, sizeof(*recs), n, out) != n) { perror(argv[3]); return 1; }
     fclose(out);
     printf("{\"frames\": %u, \"seen\": %u, \"served\": %u, \"null\": %u, \"changed\": %u, "
-           "\"rx_errors\": %llu, \"rx_packets\": %llu, \"tcp_csum_calls\": %llu, "
+           "\"rx_errors\": %llu, \"rx_packets\": %llu, \"rx_bytes\": %llu, \"tcp_csum_calls\": %llu, "
            "\"rounds\": %d, \"recv_calls\": %d, \"released\": %d, \"observe\": %d}\n",
            n, seen, served, nulls, changed, (unsigned long long)mtcp->nstat.rx_errors[0],
-           (unsigned long long)mtcp->nstat.rx_packets[0], (unsigned long long)g_csum_calls,
+           (unsigned long long)mtcp->nstat.rx_packets[0], (unsigned long long)mtcp->nstat.rx_bytes[0],
+           (unsigned long long)g_csum_calls,
            rounds, g_nic.recv_calls, g_nic.released, observe);
     free(recs);
     free(mtcp);

@@ -83,6 +83,8 @@ def test_dropin_passthrough_without_gpu(tmp_path, golden):
     tcp = ok & (br == BR_TCP_OK)
     assert np.array_equal(r["key"][tcp], flow_keys(golden)[tcp])
     assert stats["rx_errors"] == int((r["ret"] == -1).sum())
+    assert stats["rx_packets"] == n
+    assert stats["rx_bytes"] == int(golden.desc["len"].astype(np.int64).sum()) + 24 * n
     # a served frame differs from the original only where the reference, on
     # the ref-UB frame before it, zeroed a tcph->check that lies past that
     # frame (tcp_in.c:1171 with ihl pointing past len)
@@ -118,6 +120,10 @@ def test_dropin_at_the_reference_call_sites(tmp_path, golden, mode, pipeline):
     want_err = int((ok & np.isin(br, [BR_IP_SHORT, BR_IP_CSUM_BAD, BR_TCP_LEN_BAD,
                                       BR_TCP_CSUM_BAD])).sum()) + int(ub.sum())
     assert stats["rx_errors"] == want_err
+    # NETSTAT: every frame counted in rx_packets / rx_bytes, as the
+    # --disable-hwcsum path's ProcessPacket counts it (eth_in.c:20-23)
+    assert stats["rx_packets"] == n
+    assert stats["rx_bytes"] == int(golden.desc["len"].astype(np.int64).sum()) + 24 * n
     assert stats["changed"] == 0
     if mode == "observe":
         # ip_in.c:28-31 asked for every served IPv4 frame past the tot_len

@@ -76,3 +76,30 @@ def test_descriptor_past_the_buffer_is_a_verdict_not_a_fault(ctx):
     assert past.sum() > n // 7
     assert (v[past] == 11).all()                     # MTCP_GPU_V_BAD_DESC
     assert (v[~past] != 11).all()
+
+
+def test_context_on_another_device_orders_on_its_own_stream():
+    """a Context opened on device d, called with stream=None while
+    another device is current, queues its kernel on device d's current stream
+    and gives the oracle's records (needs two GPUs; the pool's boxes have one)."""
+    import numpy as np
+    import torch
+    import oracle
+    from mtcp_amd import RESULT_DTYPE, gpu, pktgen
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU visible")
+    d = torch.cuda.device_count() - 1
+    n, seed = 4096, 9
+    desc, nbytes = pktgen.layout(n, 1500, 6, seed)
+    dev = torch.device("cuda", d)
+    b = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    dd = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+    out = torch.zeros(n * 40, dtype=torch.uint8, device=dev)
+    torch.cuda.set_device(0)
+    gpu.pktgen_dev(b, dd, n, 6, seed, stream=torch.cuda.current_stream(d))
+    with gpu.Context(d) as ctx:
+        ctx.rx_chunk_dev(b, dd, n, 6, out)
+        torch.cuda.synchronize(d)
+    got = out.cpu().numpy().view(RESULT_DTYPE)
+    want = oracle.rx_chunk(b.cpu().numpy(), desc, 6)
+    assert got.tobytes() == want.tobytes()

@@ -67,7 +67,7 @@ def rx_drops(golden):
 def test_module_compiles_against_mtcp_headers(tmp_path):
     # the flags of mtcp/src/Makefile.in:20-31 (-Werror included)
     cmd = ["gcc", "-std=gnu99", "-O3", "-m64", "-Wall", "-Werror", "-fgnu89-inline", "-fcommon",
-           "-DDISABLE_PSIO", "-DDISABLE_NETMAP", "-DDISABLE_DPDK",
+           "-DNETSTAT", "-DDISABLE_PSIO", "-DDISABLE_NETMAP", "-DDISABLE_DPDK",
            "-I" + os.path.join(REF, "mtcp", "src", "include"),
            "-I" + os.path.join(REF, "io_engine", "include"), "-I" + os.path.join(ROOT, "include"),
            "-c", os.path.join(ROOT, "mtcp_amd", "io_module", "gpu_module.c"),
