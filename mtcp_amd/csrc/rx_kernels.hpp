@@ -503,12 +503,16 @@ __device__ __forceinline__ void finish_seg(Pkt &k, uint32_t seg) {
 // COMMON: the common frame on parse_common's straight path first (the
 // grouped kernels; rx_kernel's RSS instantiations have no registers left for
 // both paths).
-template <int MODE, int S, bool COMMON = false>
+// ALIGNED: the caller knows the frame starts on a 4-byte boundary (p & 3 == 0,
+// every frame of a PSIO chunk): packet dword i is raw dword a + i, no funnel
+// shift and one LDS read per dword.
+template <int MODE, int S, bool COMMON = false, bool ALIGNED = false>
 __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, uint64_t p,
                                             uint32_t L, uint32_t nch, bool desc_ok) {
     const uint32_t sh = (uint32_t)(p & 15);
     const uint32_t a = sh >> 2, fb = 8 * (sh & 3);
     auto pd = [&](uint32_t i) -> uint32_t {      // packet dword i (bytes 4i..4i+3)
+        if constexpr (ALIGNED) return raw[(a + i) * S];
         return __builtin_amdgcn_alignbit(raw[(a + i + 1) * S], raw[(a + i) * S], fb);
     };
     auto ipsum = [&](uint32_t ihl) -> uint32_t {  // words [14, 14 + 4*ihl): dwords 3..3+ihl
@@ -543,7 +547,7 @@ __device__ __forceinline__ Pkt parse_finish(const uint32_t *raw, uint32_t sum, u
 #pragma unroll
         for (uint32_t i = 0; i < 3; ++i)
             if (i < a) s_out = halves(raw[i * S], s_out);
-        if (sh & 2) s_out += raw[a * S] & 0xFFFFu;
+        if (!ALIGNED && (sh & 2)) s_out += raw[a * S] & 0xFFFFu;
         // (b) bytes [p + E, p16 + 16*nch)
         const uint64_t p16 = p & ~15ull;
         const uint64_t e_abs = p + 14 + k.ip_len;

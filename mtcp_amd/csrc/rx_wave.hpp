@@ -336,7 +336,9 @@ struct GroupShape {
 };
 
 // ABL (profiling only, tools/wave_probe.hip): 1 = phase 2 stores the sum only.
-template <int MODE, bool RSS, int G, int ABL = 0>
+// AL: phase 2 takes parse_finish's ALIGNED form when every frame of the wave
+// starts on a 4-byte boundary (AL 0: never; an A/B baseline).
+template <int MODE, bool RSS, int G, int ABL = 0, int AL = 1>
 __global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
     using Sh = GroupShape<G>;
     constexpr int P = Sh::P, U = Sh::U, R = Sh::R, S = Sh::S;
@@ -431,7 +433,11 @@ __global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
         kp.out[kk].saddr = sum;
         return;
     }
-    const Pkt pk = parse_finish<MODE, S, true>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);
+    Pkt pk;
+    if (AL && __ballot((pq & 3) != 0) == 0)
+        pk = parse_finish<MODE, S, true, true>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);
+    else
+        pk = parse_finish<MODE, S, true, false>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);
     if constexpr (is_tx(MODE)) {
         const uint32_t checks = fold_csum(pk.s_ip - pk.ip_check) | (pk.tcp_csum << 16);
         if (kp.tx_report) {

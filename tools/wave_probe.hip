@@ -60,6 +60,8 @@ int main(int argc, char **argv) {
         {"g16_p1", mg::rx_group_kernel<mg::kRxChunk, false, 16, 1>, 1024, 64},
         {"g16", mg::rx_group_kernel<mg::kRxChunk, false, 16>, 1024, 64},
         {"g4", mg::rx_group_kernel<mg::kRxChunk, false, 4>, 1024, 256},
+        {"g4noal", mg::rx_group_kernel<mg::kRxChunk, false, 4, 0, 0>, 1024, 256},
+        {"g16noal", mg::rx_group_kernel<mg::kRxChunk, false, 16, 0, 0>, 1024, 64},
         {"rows", mg::rx_kernel<mg::kRxChunk, false, mg::kSchedSorted>, 256, 0},
     };
     for (uint32_t n : ns) {
