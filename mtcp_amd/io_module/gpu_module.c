@@ -131,6 +131,8 @@ struct gpu_private_context {
     int passthrough;                      /* no GPU at init: the inner backend */
     int pipeline;                         /* serve aggregate k while k+1 is checked */
     int tx;                               /* tx checksums filled here        */
+    long fail_after;                      /* MTCP_GPU_FAIL_AFTER: fault injection, -1 off */
+    long launches;                        /* aggregates sent to the GPU       */
     struct gpu_ifq *ifq[MAX_DEVICES];     /* created at init (or first recv_pkts) */
     int ifq_failed[MAX_DEVICES];          /* no staging: this interface passes through */
     struct gpu_txq *txq[MAX_DEVICES];
@@ -257,6 +259,10 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
         return;
     g->pipeline = !(pl && strcmp(pl, "0") == 0);
     g->tx = tx && strcmp(tx, "1") == 0;
+    /* MTCP_GPU_FAIL_AFTER=k: the (k+1)-th aggregate's launch fails as a GPU
+     * error would, so the fallback to mTCP's own checksums is exercised on a
+     * healthy GPU (tests/test_dropin.py) */
+    g->fail_after = getenv("MTCP_GPU_FAIL_AFTER") ? atol(getenv("MTCP_GPU_FAIL_AFTER")) : -1;
     if (g->tx && !gpu_tx_capable(gpu_inner_module)) {
         TRACE_ERROR("gpu_module: MTCP_GPU_TX=1 refused: the wrapped backend sends from get_wptr\n");
         g->tx = 0;
@@ -415,26 +421,29 @@ static uint32_t gather(struct mtcp_thread_context *ctx, struct gpu_ifq *f, int i
     f->count[a] = total;
     f->launched[a] = 0;
     if (total && g->gpu) {
-        if (mtcp_gpu_rxq_flush_async(q) == MTCP_GPU_OK)
+        if ((g->fail_after < 0 || g->launches < g->fail_after) &&
+            mtcp_gpu_rxq_flush_async(q) == MTCP_GPU_OK) {
             f->launched[a] = 1;
-        else
+            g->launches++;
+        } else {
             gpu_fail(g);
+        }
     }
     return total;
 }
 
-/* Wait for aggregate a's verdicts (served raw if it has none). */
+/* Wait for aggregate a's verdicts (served raw if it has none).  An aggregate
+ * launched before a GPU failure keeps its verdicts: gpu_fail waited for it,
+ * and the wait here then only reads the rxq's host-side state. */
 static void finish(struct gpu_private_context *g, struct gpu_ifq *f, int a)
 {
     uint32_t n_done = 0;
     f->served_raw[a] = 1;
     if (!f->launched[a])
         return;
-    if (!g->gpu)
-        return;                       /* failed meanwhile: gpu_fail already waited */
     if (mtcp_gpu_rxq_wait(f->rxq[a], &n_done) == MTCP_GPU_OK && n_done == f->count[a])
         f->served_raw[a] = 0;
-    else
+    else if (g->gpu)
         gpu_fail(g);
 }
 
@@ -533,8 +542,8 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
         case PKT_RX_TCP_CSUM:
             /* verified on the GPU at recv time: bad frames never reach mTCP */
             f = g->ifq[nif];
-            if (f)
-                return (g->gpu && f->serving >= 0 && !f->served_raw[f->serving]) ? 0 : -1;
+            if (f)      /* the frames being served carry GPU verdicts */
+                return (f->serving >= 0 && !f->served_raw[f->serving]) ? 0 : -1;
             break;                                   /* a passthrough interface */
         case PKT_TX_TCPIP_CSUM_PEEK:
         case PKT_TX_TCPIP_CSUM:

@@ -43,13 +43,15 @@ BR_TCP_OK, BR_IP_SHORT, BR_IP_CSUM_BAD, BR_TCP_LEN_BAD, BR_TCP_CSUM_BAD = 0, 3, 
 NULL = 254
 
 
-def run_dropin(tmp_path, mode="observe", pipeline="1"):
+def run_dropin(tmp_path, mode="observe", pipeline="1", fail_after=None):
     if not os.path.exists(EXE):
         pytest.fail("oracle/_ref/dropin_rx not built: `make -C oracle ref` (needs /root/reference)")
-    out = tmp_path / f"dropin_{mode}_{pipeline}.bin"
+    out = tmp_path / f"dropin_{mode}_{pipeline}_{fail_after}.bin"
+    env = dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX="0")
+    if fail_after is not None:
+        env["MTCP_GPU_FAIL_AFTER"] = str(fail_after)
     p = subprocess.run([EXE, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
-                        str(out), mode], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX="0"))
+                        str(out), mode], capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads(p.stdout.strip().splitlines()[-1]), np.fromfile(out, dtype=REC)
 
@@ -145,6 +147,48 @@ def test_dropin_at_the_reference_call_sites(tmp_path, golden, mode, pipeline):
     padded = ok & (br == BR_TCP_OK) & (14 + tot < ln)
     assert past.sum() >= 8 and (r["branch"][past] == NULL).all()
     assert padded.sum() >= 30 and (r["branch"][padded] == BR_TCP_OK).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", ["1", "0"])
+def test_dropin_gpu_failure_falls_back_to_mtcp(tmp_path, golden, pipeline):
+    """A GPU error mid-stream (MTCP_GPU_FAIL_AFTER=1: the second aggregate's
+    launch fails): gpu_module serves the rest unchecked and answers dev_ioctl
+    -1, mTCP's own ip_fast_csum / TCPCalcChecksum take over (ip_in.c:29-31,
+    tcp_in.c:1160-1164), and the outcome of the whole run — every frame's
+    branch, return value and stream key, rx_packets / rx_bytes / rx_errors —
+    is still the --disable-hwcsum reference's (the frames of the failed part
+    are checked by the reference itself, ref-UB ones included)."""
+    stats, r = run_dropin(tmp_path, "observe", pipeline, fail_after=1)
+    n = len(golden.desc)
+    ub = golden.meta["ref_ub"] == 1
+    ok = ~ub
+    br = golden.meta["branch"]
+    assert stats["frames"] == stats["seen"] == n
+    gpu_part = r["branch"] == NULL
+    asked = r["ioctl_ip"] != -2
+    # the GPU checked a prefix (its answers 0), mTCP the rest (-1)
+    assert (r["ioctl_ip"][asked] == 0).any() and (r["ioctl_ip"][asked] == -1).any()
+    first_sw = int(np.nonzero(r["ioctl_ip"] == -1)[0][0])
+    assert (r["ioctl_ip"][:first_sw][asked[:first_sw]] == 0).all()
+    assert (r["ioctl_ip"][first_sw:][asked[first_sw:]] == -1).all()
+    assert not gpu_part[first_sw:].any()
+    assert stats["tcp_csum_calls"] > 100
+    # every defined frame: the reference's branch (NULL = its checksum drops)
+    served = ~gpu_part
+    assert np.array_equal(r["branch"][served & ok], br[served & ok])
+    assert set(br[gpu_part & ok].tolist()) <= {BR_IP_CSUM_BAD, BR_TCP_CSUM_BAD}
+    tcp = served & ok & (br == BR_TCP_OK)
+    assert np.array_equal(r["key"][tcp], flow_keys(golden)[tcp])
+    assert stats["rx_packets"] == n
+    assert stats["rx_bytes"] == int(golden.desc["len"].astype(np.int64).sum()) + 24 * n
+    # rx_errors: the reference's errors over the defined frames; a ref-UB
+    # frame counts when the GPU dropped it, or when the reference's own
+    # (undefined) reading of it returned ERROR
+    ub_err = int((ub & gpu_part).sum()) + int((ub & served & (r["ret"] == -1)).sum())
+    want_err = int((ok & np.isin(br, [BR_IP_SHORT, BR_IP_CSUM_BAD, BR_TCP_LEN_BAD,
+                                      BR_TCP_CSUM_BAD])).sum()) + ub_err
+    assert stats["rx_errors"] == want_err
 
 
 # ---- the tx side: SendTCPPacketStandalone / IPOutputStandalone ----------------
