@@ -58,3 +58,6 @@ tools/wave_probe: tools/wave_probe.hip mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/r
 
 tools/occ_probe: tools/occ_probe.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
+
+tools/tx_probe: tools/tx_probe.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
