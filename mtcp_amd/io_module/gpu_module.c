@@ -485,7 +485,9 @@ static uint8_t *gpu_get_rptr(struct mtcp_thread_context *ctx, int ifidx, int ind
     if (!f)
         return INNER_CALL(ctx, gpu_inner_module->get_rptr(ctx, ifidx, index, len));
     a = f->serving;
-    if (a < 0 || f->dropped[a][index])
+    if (a < 0 || index < 0 || (uint32_t)index >= f->count[a])
+        return NULL;                  /* not a frame of the burst recv_pkts returned */
+    if (f->dropped[a][index])
         return NULL;                  /* the wrapped backend's own NULL */
     if (f->served_raw[a])
         return mtcp_gpu_rxq_frame(f->rxq[a], (uint32_t)index, len);
