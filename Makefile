@@ -49,7 +49,7 @@ tools: tools/rx_variants tools/hbm_ceiling tools/store_probe tools/pcie_probe to
 # gpu_module.c driven by the RunMainLoop rx harness; the
 # mTCP types come from the test doubles in tests/c/mtcp_double.
 tests/c/rxloop: tests/c/rxloop.c mtcp_amd/io_module/gpu_module.c mtcp_amd/io_module/gpu_topo.h include/mtcp_gpu_rxq.h oracle/mtcp_oracle.c $(LIB)
-	gcc -std=gnu99 -O2 -Wall -pthread -Itests/c/mtcp_double -Iinclude -o $@ tests/c/rxloop.c \
+	gcc -std=gnu99 -O3 -Wall -pthread -Itests/c/mtcp_double -Iinclude -o $@ tests/c/rxloop.c \
 	    mtcp_amd/io_module/gpu_module.c oracle/mtcp_oracle.c -Lmtcp_amd/lib -lmtcp_gpu \
 	    -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib'
 

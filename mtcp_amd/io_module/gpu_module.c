@@ -62,7 +62,10 @@
  * dealt round-robin among that node's devices (gpu_topo.h; mTCP binds each
  * thread's memory to its core's node, mtcp/src/cpu.c:54-79, and DPDK puts
  * each port's queues on the NIC's socket, dpdk_module.c:660-663);
- * MTCP_GPU_DEVICE=d forces one.
+ * MTCP_GPU_DEVICE=d forces one.  MTCP_GPU_THREADS=k: only the first k
+ * threads to start on a device offload (the rest pass through and mTCP
+ * checks their frames itself): past two threads a GPU's PCIe link is full
+ * (DESIGN.md §5).
  *
  * Resources per mTCP thread: one GPU context (one HIP stream), and, for each
  * of the CONFIG.eths_num interfaces (mtcp.h:138), two rxqs (pinned staging
@@ -239,6 +242,21 @@ static int gpu_pick_device(int cpu, int ndev)
     return gpu_topo_pick(cpu, node, rank, ndev, dev_node);
 }
 
+/* MTCP_GPU_THREADS=k: at most k mTCP threads per GPU offload; the others
+ * run on the wrapped backend alone (dev_ioctl -1: mTCP's own checksums).
+ * One GPU's PCIe link carries the frames of about two threads (DESIGN.md
+ * §5), so threads beyond that wait on the link while their cores could
+ * check frames themselves.  Unset: every thread offloads. */
+static int gpu_thread_count[GPU_TOPO_MAX_DEVS];
+
+static int gpu_thread_admitted(int dev)
+{
+    const char *lim = getenv("MTCP_GPU_THREADS");
+    if (!lim || !*lim || dev >= GPU_TOPO_MAX_DEVS)
+        return 1;
+    return __sync_fetch_and_add(&gpu_thread_count[dev], 1) < atoi(lim);
+}
+
 static void gpu_init_handle(struct mtcp_thread_context *ctx)
 {
     struct gpu_private_context *g = calloc(1, sizeof(*g));
@@ -270,6 +288,10 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 
     ndev = mtcp_gpu_device_count();
     dev = ndev > 0 ? gpu_pick_device(ctx->cpu, ndev) : -1;
+    if (dev >= 0 && !gpu_thread_admitted(dev)) {
+        g->passthrough = 1;                  /* mTCP's own checksums on this core */
+        return;
+    }
     /* compact 16 B records: the rxqs read the verdict only (40 -> 16 B of D2H per frame) */
     if (dev < 0 || mtcp_gpu_open(&g->gpu, dev, NULL, 1, MTCP_GPU_F_COMPACT) != MTCP_GPU_OK ||
         mtcp_gpu_reserve(g->gpu, 0, 0) != MTCP_GPU_OK) {     /* load the kernels now */

@@ -234,10 +234,23 @@ static void *worker_main(void *arg)
         }
         idle = 0;
         w->rounds++;
+        /* timing modes: where the module answers -1 (a thread it does not
+         * offload, MTCP_GPU_THREADS), ProcessPacket runs mTCP's own checks
+         * (ip_in.c:35-36, tcp_in.c:1165-1173): the harness pays for them
+         * with the restated chain and drops what they drop */
+        const int sw = w->timing && gpu_module_func.dev_ioctl(&ctx, 0, PKT_RX_TCP_CSUM, NULL) == -1;
         for (i = 0; i < recv_cnt; i++) {
             uint16_t len = 0;
             uint8_t *pktbuf = gpu_module_func.get_rptr(&ctx, 0, i, &len);
             const mtcp_gpu_desc *d = &f->desc[w->seen + (uint32_t)i];
+            if (pktbuf != NULL && sw) {
+                mtcp_gpu_result r;
+                const int v = oracle_rx_packet(pktbuf, len, NULL, &r);
+                if (v == MTCP_GPU_V_IP_CSUM_BAD || v == MTCP_GPU_V_TCP_CSUM_BAD || v == MTCP_GPU_V_TRUNCATED)
+                    pktbuf = NULL;                     /* ERROR: counted in rx_errors */
+                else
+                    w->hdr_sum += r.ip_csum + r.tcp_csum;
+            }
             if (pktbuf != NULL) {
                 /* ProcessPacket(mtcp, rx_inf, ts, pktbuf, len) would run here */
                 if (w->timing == 1) {
@@ -288,6 +301,7 @@ int main(int argc, char **argv)
     const mtcp_gpu_desc *desc;
     uint32_t n, seen = 0;
     uint64_t rx_packets = 0, rx_errors = 0, changed = 0, hdr_sum = 0, frame_bytes = 0;
+    int offloading = 0;                               /* threads whose dev_ioctl answered 0 */
     int rounds = 0, recv_calls = 0, timing, threads, t;
     struct timespec t1;
     struct worker *ws;
@@ -359,6 +373,7 @@ int main(int argc, char **argv)
         changed += w->changed;
         hdr_sum += w->hdr_sum;
         rounds += w->rounds;
+        offloading += w->ioctl_tcp == 0;
         recv_calls += w->fake.recv_calls;
         seen += w->seen;
         if (t == 0 || w->t1.tv_sec > t1.tv_sec ||
@@ -395,11 +410,12 @@ int main(int argc, char **argv)
     printf("{\"frames\": %u, \"seen\": %u, \"rounds\": %d, \"inner_bursts\": %d, "
            "\"rx_packets\": %llu, \"rx_errors\": %llu, \"changed\": %llu, "
            "\"ioctl_rx_ip\": %d, \"ioctl_rx_tcp\": %d, \"seconds\": %.6f, "
-           "\"frame_bytes\": %llu, \"timing_mode\": %d, \"hdr_sum\": %llu, \"threads\": %d}\n",
+           "\"frame_bytes\": %llu, \"timing_mode\": %d, \"hdr_sum\": %llu, \"threads\": %d, "
+           "\"offloading_threads\": %d}\n",
            n, seen, rounds, recv_calls, (unsigned long long)rx_packets,
            (unsigned long long)rx_errors, (unsigned long long)changed, ws[0].ioctl_ip,
            ws[0].ioctl_tcp, secs, (unsigned long long)frame_bytes, timing,
-           (unsigned long long)hdr_sum, threads);
+           (unsigned long long)hdr_sum, threads, offloading);
     free(ws);
     free(status);
     free((void *)buf);

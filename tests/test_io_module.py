@@ -33,13 +33,13 @@ def build_rxloop() -> str:
     return os.path.join(ROOT, "tests", "c", "rxloop")
 
 
-def run_rxloop(tmp_path, threads=1, pipeline="1", mode="verify", tx="0", as_netmap="0"):
+def run_rxloop(tmp_path, threads=1, pipeline="1", mode="verify", tx="0", as_netmap="0", env=None):
     exe = build_rxloop()
     status = tmp_path / "status.bin"
     p = subprocess.run([exe, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
                         str(status), mode, str(threads)], capture_output=True, text=True,
                        timeout=300, env=dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX=tx,
-                                             RXLOOP_AS_NETMAP=as_netmap))
+                                             RXLOOP_AS_NETMAP=as_netmap, **(env or {})))
     assert p.returncode == 0, p.stderr
     return json.loads(p.stdout.strip().splitlines()[-1]), np.fromfile(status, dtype=np.uint8)
 
@@ -90,6 +90,20 @@ def test_passthrough_without_gpu(tmp_path):
     assert stats["ioctl_rx_ip"] == -1 and stats["ioctl_rx_tcp"] == -1
 
 
+def test_passthrough_timing_mode_checks_in_software(tmp_path, golden):
+    """Where the module answers dev_ioctl -1, the harness's timing modes run
+    mTCP's own checks (the restated chain) on every served frame and drop what
+    ProcessPacket drops: the same frames the GPU path serves as NULL."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    stats, status = run_rxloop(tmp_path, threads=2, mode="timing")
+    drop = rx_drops(golden)
+    assert stats["offloading_threads"] == 0
+    assert np.array_equal(status == 0, drop)
+    assert stats["rx_errors"] == int(drop.sum()) > 100
+
+
 def test_tx_passthrough_without_gpu(tmp_path, golden):
     import torch
     if torch.cuda.is_available():
@@ -134,6 +148,20 @@ def test_gpu_module_one_context_per_thread(tmp_path, golden, pipeline):
     assert (status[~drop] == 1).all() and stats["changed"] == 0
     assert stats["rx_errors"] == int(drop.sum())
     assert stats["ioctl_rx_ip"] == 0 and stats["ioctl_rx_tcp"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("limit", ["0", "2", "4"])
+def test_gpu_threads_limit_splits_the_checks(tmp_path, golden, limit):
+    """MTCP_GPU_THREADS=k: k of the four threads offload, the others run on
+    the wrapped backend alone and mTCP's own checks run there (the harness's
+    timing mode pays for them): every thread drops the same frames."""
+    stats, status = run_rxloop(tmp_path, threads=4, mode="timing", env={"MTCP_GPU_THREADS": limit})
+    drop = rx_drops(golden)
+    assert stats["offloading_threads"] == int(limit)
+    assert stats["seen"] == stats["frames"] == len(golden.desc)
+    assert np.array_equal(status == 0, drop)
+    assert stats["rx_errors"] == int(drop.sum())
 
 
 @pytest.mark.gpu

@@ -158,6 +158,42 @@ def main():
         seeds = {64: 1, 1500: 2, "bimodal": 3}
         dump(n, size, seeds.get(size, 7), sys.argv[3])
         return
+    if "--hybrid" in sys.argv:
+        # MTCP_GPU_THREADS=k (gpu_module.c): k threads offload, the others
+        # check in software (rxloop's timing mode pays mTCP's own checks
+        # where dev_ioctl answers -1); every thread and the reference's own
+        # rx code pinned to the CPUs of the GPU's NUMA node; interleaved
+        host = host_topology()
+        print(json.dumps(host), flush=True)
+        local = host["gpu_local_cpus"]
+        saved = os.sched_getaffinity(0)
+        with tempfile.TemporaryDirectory() as tmp:
+            for size in (1500, 64):
+                seed = 2 if size == 1500 else 1
+                for rep in range(2):
+                    for threads in (4, 8, 16):
+                        for limit in ("all", "0", "1", "2", "4"):
+                            os.environ["RXLOOP_CPUS"] = ",".join(map(str, local))
+                            os.environ.pop("MTCP_GPU_THREADS", None)
+                            if limit != "all":
+                                os.environ["MTCP_GPU_THREADS"] = limit
+                            r = run(n, size, seed, tmp, "timing", threads, True)
+                            print(json.dumps({"probe": "io_hybrid", "rep": rep, "frame_size": size,
+                                              "threads": threads, "gpu_threads": limit,
+                                              "frames": n, "mpkt_per_s": r["mpkt_per_s"],
+                                              "GBs": r["GBs"], "rx_errors": r["rx_errors"]}),
+                                  flush=True)
+                os.environ.pop("MTCP_GPU_THREADS", None)
+                os.environ.pop("RXLOOP_CPUS", None)
+                os.sched_setaffinity(0, local)
+                try:
+                    ref = reference(n, size, seed)
+                finally:
+                    os.sched_setaffinity(0, saved)
+                if ref:
+                    ref["pinned"] = "gpu_local_cpus"
+                    print(json.dumps(ref), flush=True)
+        return
     if "--threads-sweep" in sys.argv:
         # thread scaling at 1500 B, timing mode: threads pinned to CPUs of
         # the GPU's NUMA node, pinned to the first CPUs the process may use
