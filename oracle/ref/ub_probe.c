@@ -25,7 +25,16 @@
  *            read past len counts, even when this frame's outcome happens not
  *            to depend on the byte (e.g. tot_len's low byte compared with 20).
  *
- * ref-UB by observation = strict fault and not a masked tail.  The reads
+ *   write    the first access past len is a store, not a load: the
+ *            `tcph->check = 0` of a TCP_CSUM_BAD frame whose TCP header is
+ *            shorter than 18 bytes at the frame's end (doff < 5 and tot_len
+ *            covering only 4*doff bytes: mtcp/src/tcp_in.c:1171).  Every read
+ *            was inside the frame and the branch is decided: re-run with 64
+ *            readable bytes after it, the branch must be TCP_CSUM_BAD.  The
+ *            reference corrupts two bytes after the frame there (the GPU path
+ *            writes nothing); its result is defined.
+ *
+ * ref-UB by observation = strict fault, not a masked tail, not a write.  The reads
  * that define it are ip_fast_csum's 4*ihl bytes (io_engine/include/ps.h:
  * 66-95), the header fields ProcessPacket / ProcessIPv4Packet /
  * ProcessTCPPacket load (eth_in.c:13, ip_in.c:19-20, tcp_in.c:1141-1152),
@@ -33,7 +42,7 @@
  *
  * usage: ub_probe GOLDEN_DIR OUT_FILE
  * OUT_FILE: one byte per golden frame — bit 0 strict fault, bit 1 masked
- * tail, bit 2 ref-UB by observation; bits 3-7 zero.  Prints a JSON summary.
+ * tail, bit 2 ref-UB by observation, bit 3 write past len; bits 4-7 zero.  Prints a JSON summary.
  * tests/test_oracle_golden.py::test_ref_ub_is_what_the_reference_reads_past_len
  * asserts bit 2 == (rx_meta ref_ub == 1) for every frame.
  */
@@ -45,6 +54,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <ucontext.h>
 #include <unistd.h>
 
 #include "ref_glue.h"
@@ -53,11 +63,18 @@
 
 static sigjmp_buf g_env;
 static volatile uintptr_t g_fault_addr;
+static volatile int g_fault_write;          /* the faulting access was a store */
 
 static void on_fault(int sig, siginfo_t *si, void *uc)
 {
-    (void)sig; (void)uc;
+    (void)sig;
     g_fault_addr = (uintptr_t)si->si_addr;
+#ifdef REG_ERR
+    /* x86-64 page-fault error code: bit 1 set for a write access */
+    g_fault_write = (((ucontext_t *)uc)->uc_mcontext.gregs[REG_ERR] & 2) != 0;
+#else
+    g_fault_write = 0;
+#endif
     siglongjmp(g_env, 1);
 }
 
@@ -66,7 +83,7 @@ static void on_fault(int sig, siginfo_t *si, void *uc)
  * (golden_gen.c takes it for every IPv4 frame past the ip_len < 20 test) and
  * the stream key StreamHTSearch received */
 typedef struct {
-    int faulted, br, ret;
+    int faulted, fault_write, br, ret;
     uint16_t csum, ip_csum;
     uint8_t key[12];
     long fault_off;
@@ -105,6 +122,7 @@ static run_t run_ref(uint8_t *guard, const uint8_t *frame0, uint32_t len, uint32
         faulted = 1;
     }
     r.faulted = faulted;
+    r.fault_write = faulted && g_fault_write;
     r.fault_off = faulted ? (long)((intptr_t)g_fault_addr - (intptr_t)p) : -1;
     return r;
 }
@@ -147,7 +165,7 @@ int main(int argc, char **argv)
     uint8_t *buf, *map, *guard, *out;
     const ref_desc_t *desc;
     const uint8_t *meta;
-    uint32_t n, i, strict = 0, masked = 0, ub = 0, agree = 0, fault_at_len = 0;
+    uint32_t n, i, strict = 0, masked = 0, ub = 0, agree = 0, fault_at_len = 0, writes = 0;
     struct sigaction sa;
     FILE *f;
 
@@ -179,13 +197,18 @@ int main(int argc, char **argv)
         const uint8_t *frame = buf + desc[i].offset;
         uint32_t len = desc[i].len;
         run_t s;
-        int is_masked = 0, is_ub;
-        if (desc[i].offset + (size_t)len > nb || len + 1 > (uint32_t)(DATA_PAGES * pg)) {
+        int is_masked = 0, is_write = 0, is_ub;
+        if (desc[i].offset + (size_t)len > nb || len + 64 > (uint32_t)(DATA_PAGES * pg)) {
             fprintf(stderr, "ub_probe: frame %u out of range\n", i);
             return 1;
         }
         s = run_ref(guard, frame, len, 0, 0);
-        if (s.faulted) {
+        if (s.faulted && s.fault_write) {
+            run_t w = run_ref(guard, frame, len, 64, 0);
+            is_write = !w.faulted && w.br == REF_BR_TCP_CSUM_BAD;
+            strict++;
+            fault_at_len += s.fault_off == (long)len;
+        } else if (s.faulted) {
             static const uint8_t fills[4] = {0x00, 0xFF, 0x5A, 0xA5};
             run_t a = run_ref(guard, frame, len, 1, fills[0]);
             int k;
@@ -198,17 +221,18 @@ int main(int argc, char **argv)
             strict++;
             fault_at_len += s.fault_off == (long)len;
         }
-        is_ub = s.faulted && !is_masked;
+        is_ub = s.faulted && !is_masked && !is_write;
         masked += is_masked;
+        writes += is_write;
         ub += is_ub;
         agree += is_ub == (meta[4 * i] == 1);
-        out[i] = (uint8_t)(s.faulted | is_masked << 1 | is_ub << 2);
+        out[i] = (uint8_t)(s.faulted | is_masked << 1 | is_ub << 2 | is_write << 3);
     }
     f = fopen(argv[2], "wb");
     if (!f || fwrite(out, 1, n, f) != n) { perror(argv[2]); return 1; }
     fclose(f);
     printf("{\"frames\": %u, \"strict_faults\": %u, \"fault_at_len\": %u, \"masked_tail\": %u, "
-           "\"ref_ub_observed\": %u, \"agree_with_meta\": %u}\n",
-           n, strict, fault_at_len, masked, ub, agree);
+           "\"write_past_len\": %u, \"ref_ub_observed\": %u, \"agree_with_meta\": %u}\n",
+           n, strict, fault_at_len, masked, writes, ub, agree);
     return 0;
 }

@@ -162,6 +162,42 @@ def test_ref_ub_at_mtcp_build_flags(golden):
     assert not (p3 & 2).any()
 
 
+def test_ub_probe_tells_a_write_past_len_from_a_read(tmp_path):
+    """A TCP frame whose header ends before the check field's end (doff 4,
+    tot_len covering 16 TCP bytes, frame ending there) and whose checksum
+    fails: every read of the reference is inside the frame and its branch is
+    TCP_CSUM_BAD, then `tcph->check = 0` (tcp_in.c:1171) stores two bytes past
+    it.  The probe reports that store (bit 3), not ref-UB, and the oracle's
+    verdict is TCP_CSUM_BAD (found by tools/oracle_soak.py)."""
+    import os
+    import subprocess
+    import oracle
+    from mtcp_amd import DESC_DTYPE
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exes = [os.path.join(root, "oracle", "_ref", e) for e in ("ub_probe_O0", "ub_probe")]
+    if not all(os.path.exists(e) for e in exes):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    f = np.zeros(64, np.uint8)
+    f[12:14] = (0x08, 0x00)
+    f[14], f[16], f[17], f[22], f[23] = 0x45, 0, 36, 64, 6
+    f[26:34] = (10, 0, 0, 1, 10, 0, 0, 2)
+    f[24:26] = 0
+    c = oracle.ip_fast_csum(f[14:34].tobytes(), 5)
+    f[24], f[25] = c & 0xFF, c >> 8
+    f[34 + 12] = 0x40                                   # doff 4
+    desc = np.zeros(1, dtype=DESC_DTYPE)
+    desc["len"] = 50                                    # 14 + tot_len
+    assert oracle.rx_chunk(f, desc, 0)["verdict"][0] == 9        # TCP_CSUM_BAD
+    f.tofile(tmp_path / "rx_buf.bin")
+    desc.tofile(tmp_path / "rx_desc.bin")
+    np.zeros(4, np.uint8).tofile(tmp_path / "rx_meta.bin")       # not ref-UB
+    for exe in exes:
+        r = subprocess.run([exe, str(tmp_path), str(tmp_path / "ub.bin")], check=True,
+                           capture_output=True, text=True, timeout=60)
+        assert '"write_past_len": 1' in r.stdout and '"agree_with_meta": 1' in r.stdout, r.stdout
+        assert np.fromfile(tmp_path / "ub.bin", np.uint8)[0] == 1 | 8
+
+
 def test_ub_probe_reproduces(golden, tmp_path):
     """Where the reference build is present, re-run the probe: it writes the
     committed bytes."""
