@@ -379,9 +379,11 @@ def run_row(args):
         algo = n * (40 + 4)
         line.update(value=round(n / wall / 1e9, 4), unit="Gpkt/s", dtype="u32",
                     ms_per_step=round(wall * 1e3, 5))
+        traffic, traffic_note = pmc_traffic("f3")
         line["roofline"] = {"bound": "hbm", "achieved": round(algo / kern / 1e9, 2),
                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                            "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                            "traffic_source": traffic_note, "kernel": "mg::flow_hash_kernel",
                             "avg_launch_ms": round(kern * 1e3, 5),
                             "algorithmic_bytes_per_launch": algo,
                             "note": "40 B record read (its 12 key bytes and verdict span the "

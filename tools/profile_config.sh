@@ -4,7 +4,7 @@
 #   2. --pmc FETCH_SIZE          3. --pmc WRITE_SIZE
 #   4. --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum
 # usage: tools/profile_config.sh CONFIG OUTDIR
-#   CONFIG: c2 c3 c5 (bench configs), c3_compact (c3 with 16 B records), f1
+#   CONFIG: c1 c2 c3 c5 (bench configs), c3_compact (c3 with 16 B records), f1, f3
 cfg=$1; out=$2
 mkdir -p "$out"
 export TMPDIR=/tmp

@@ -3,7 +3,7 @@
 # time limit (tools/gpu_steps.sh stops at the first fault or timeout):
 #   /usr/local/graft/bin/gpurun --timeout 1150 -- 'bash tools/round_evidence.sh'
 # then, back in the build container:
-#   python3 tools/update_profiles.py rNN c2 c3 c3_compact c5 f1   (+ copy the row / probe outputs)
+#   python3 tools/update_profiles.py rNN c1 c2 c3 c3_compact c5 f1 f3   (+ copy the row / probe outputs)
 # Order: the PMC passes first, then `update_profiles.py --traffic` writes
 # profiles/traffic_<cfg>.json for THIS build, then the bench lines, so every
 # committed bench line quotes the traffic of the library it measured.
@@ -15,7 +15,9 @@ bash tools/gpu_steps.sh \
   "p3c|200|bash tools/profile_config.sh c3_compact gpurun_out/prof_c3_compact" \
   "p5|240|bash tools/profile_config.sh c5 gpurun_out/prof_c5" \
   "pf1|200|bash tools/profile_config.sh f1 gpurun_out/prof_f1" \
-  "tr|60|python3 tools/update_profiles.py --traffic c2 c3 c3_compact c5 f1" \
+  "p1|200|bash tools/profile_config.sh c1 gpurun_out/prof_c1" \
+  "pf3|200|bash tools/profile_config.sh f3 gpurun_out/prof_f3" \
+  "tr|60|python3 tools/update_profiles.py --traffic c1 c2 c3 c3_compact c5 f1 f3" \
   "bc1|150|python bench.py --config c1" \
   "bc2|150|python bench.py --config c2" \
   "bc3|150|python bench.py --config c3" \

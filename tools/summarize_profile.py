@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarize tools/profile_config.sh output for one config into a JSON file
-for profiles/: rx_kernel average duration (kernel trace), HBM traffic per
+for profiles/: the config's kernel's average duration (kernel trace), HBM traffic per
 launch from PMC (FETCH_SIZE x 2 per the gfx950 correction of
 MI355X_MICROARCH.md §HBM, cross-checked against TCC_EA0_RDREQ_128B x 128 B;
 WRITE_SIZE as is), and the algorithmic bytes."""
@@ -12,8 +12,11 @@ import sys
 
 src, cfg, out = sys.argv[1], sys.argv[2], sys.argv[3]
 # algorithmic bytes per launch: sum L (rx), sum L + 4 B of check fields per frame (f1)
-algo = {"c2": 1572864000, "c3": 819090368, "c3_compact": 819090368, "c5": 4718592000,
-        "f1": 1572864000 + 4 * (1 << 20)}[cfg]
+algo = {"c1": 65536 * 64, "c2": 1572864000, "c3": 819090368, "c3_compact": 819090368, "c5": 4718592000,
+        "f1": 1572864000 + 4 * (1 << 20), "f3": (1 << 20) * (40 + 4)}[cfg]
+# the config's dominant kernel: C1's 64 K small frames take the quad kernel
+# (mtcp_gpu.hip pick_sched), f3 is the separate HashFlow kernel
+KERNEL = {"c1": "rx_group_kernel", "f3": "flow_hash_kernel"}.get(cfg, "rx_kernel")
 
 
 def rows(pattern):
@@ -28,8 +31,8 @@ def kname(r):
 
 
 stats = {r["Name"]: r for r in rows(f"{src}/trace/run_kernel_stats.csv")}
-rx = [k for k in stats if k.startswith("rx_kernel")][0]
-trace = [r for r in rows(f"{src}/trace/run_kernel_trace.csv") if kname(r).startswith("rx_kernel")]
+rx = [k for k in stats if k.startswith(KERNEL)][0]
+trace = [r for r in rows(f"{src}/trace/run_kernel_trace.csv") if kname(r).startswith(KERNEL)]
 trace.sort(key=lambda r: int(r["Start_Timestamp"]))
 durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace]
 # the bench's own line under the profiler (same process): HIP-event average
@@ -45,7 +48,7 @@ timed = durs[-steps:]
 
 def pmc(sub, counter):
     v = [float(r["Counter_Value"]) for r in rows(f"{src}/{sub}/run_counter_collection.csv")
-         if kname(r).startswith("rx_kernel") and r["Counter_Name"] == counter]
+         if kname(r).startswith(KERNEL) and r["Counter_Name"] == counter]
     return statistics.median(v) if v else None
 
 
@@ -67,9 +70,9 @@ res = {
     "timed_steps": len(timed),
     "timed_avg_duration_ns": statistics.mean(timed),
     "bench_events_avg_launch_ns_same_run": bench["roofline"]["avg_launch_ms"] * 1e6 if bench else None,
-    "note_launches": "all rx_kernel launches of the run: the generator's tx fill (pktgen uses the "
-                     "kernel in fill mode), the warm-up steps and the timed steps; timed_* = the "
-                     "last `steps` launches, the ones bench.py's HIP events bracket",
+    "note_launches": f"all {KERNEL} launches of the run (for rx_kernel: the generator's tx fill, "
+                     "pktgen uses the kernel in fill mode), the warm-up steps and the timed steps; "
+                     "timed_* = the last `steps` launches, the ones bench.py's HIP events bracket",
     "stats_row": stats[rx],
     "algorithmic_bytes_per_launch": algo,
     "achieved_GBs_from_trace": algo / statistics.median(durs),
