@@ -78,6 +78,7 @@ extern "C" {
 #define MTCP_GPU_ENOMEM   (-12)  /* device or pinned host allocation failed  */
 #define MTCP_GPU_ENODEV   (-19)  /* no such HIP device / no GPU              */
 #define MTCP_GPU_EIO       (-5)  /* HIP runtime error during the call        */
+#define MTCP_GPU_ETIMEDOUT (-110) /* the GPU did not finish within the limit the caller set */
 
 /* ---- dev_ioctl commands: same values as mtcp/src/include/io_module.h:80-87 */
 #define MTCP_GPU_PKT_TX_IP_CSUM          0x01
@@ -386,6 +387,11 @@ int mtcp_gpu_host_unregister(void *ptr);
 
 /* Synchronise the context's stream. */
 int mtcp_gpu_sync(mtcp_gpu_ctx *ctx);
+
+/* Fault injection for tests of a caller's hang handling: queue a kernel on
+ * the context's stream that keeps it busy for `us` microseconds (at most
+ * 10 s), so that work queued behind it completes that much later. */
+int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us);
 
 #ifdef __cplusplus
 }

@@ -75,6 +75,13 @@ int  mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n);
 int  mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q);
 int  mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n);
 
+/* rxq_wait with a limit (timeout_us 0: none).  If the results are not in
+ * after timeout_us, the flush is abandoned and MTCP_GPU_ETIMEDOUT returned:
+ * its frames stay staged (served by rxq_frame, without verdicts), the rxq
+ * takes resets and pushes again, but no further flush (MTCP_GPU_EIO: the
+ * abandoned flush may still write its results). */
+int  mtcp_gpu_rxq_wait_for(mtcp_gpu_rxq *q, uint32_t *n, uint32_t timeout_us);
+
 /* get_rptr for flushed frame i: the staged frame and its length, or NULL for
  * the verdicts listed above.  *res (may be NULL) receives the frame's result
  * record: a mtcp_gpu_result, or — when the rxq's context was opened with

@@ -17,6 +17,7 @@
 #include <stddef.h>
 #include <string.h>
 
+#include <chrono>
 #include <new>
 
 #include "../../include/mtcp_gpu.h"
@@ -44,6 +45,7 @@ struct mtcp_gpu_rxq {
     uint32_t n = 0;                      // frames staged
     uint32_t done_n = 0;                 // frames with results
     uint32_t inflight = 0;               // frames of an unfinished flush_async (0: none)
+    bool abandoned = false;              // a flush timed out in rxq_wait_for: no more flushes
     uint64_t used = 0;                   // staging bytes in use
     // A/B knobs (environment at create): MTCP_GPU_STAGE=plain copies frames
     // with memcpy (cached stores) instead of streaming stores;
@@ -186,6 +188,7 @@ uint32_t mtcp_gpu_rxq_pending(const mtcp_gpu_rxq *q) { return q ? q->n - q->done
 
 int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
     if (!q || q->inflight) return MTCP_GPU_EINVAL;
+    if (q->abandoned) return MTCP_GPU_EIO;
     if (q->n == q->done_n) return MTCP_GPU_OK;
     RxqDevice dg(q->device);
     if (!dg.ok) return MTCP_GPU_ENODEV;
@@ -226,6 +229,33 @@ int mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n) {
             rc = MTCP_GPU_EIO;
         q->inflight = 0;
     }
+    if (n) *n = q->done_n;
+    return rc;
+}
+
+int mtcp_gpu_rxq_wait_for(mtcp_gpu_rxq *q, uint32_t *n, uint32_t timeout_us) {
+    if (!q) return MTCP_GPU_EINVAL;
+    if (!q->inflight || timeout_us == 0) return mtcp_gpu_rxq_wait(q, n);
+    RxqDevice dg(q->device);
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+    int rc = MTCP_GPU_OK;
+    for (;;) {
+        const hipError_t e = hipEventQuery(q->evt);
+        if (e == hipSuccess) {
+            q->done_n += q->inflight;
+            break;
+        }
+        if (e != hipErrorNotReady) {
+            rc = MTCP_GPU_EIO;
+            break;
+        }
+        if (std::chrono::steady_clock::now() >= deadline) {
+            q->abandoned = true;              // its results may still arrive: never read them
+            rc = MTCP_GPU_ETIMEDOUT;
+            break;
+        }
+    }
+    q->inflight = 0;
     if (n) *n = q->done_n;
     return rc;
 }

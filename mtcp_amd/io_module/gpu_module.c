@@ -38,7 +38,10 @@
  * dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers 0 while the GPU path
  * of that interface is healthy and -1 otherwise, so mTCP falls back to its
  * own checksums exactly as with a NIC that lacks the offload
- * (dpdk_dev_ioctl, dpdk_module.c:809-816).
+ * (dpdk_dev_ioctl, dpdk_module.c:809-816).  Every wait for an aggregate is
+ * bounded (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000, 0: none): a GPU that
+ * stops answering is abandoned, never waited on again, and mTCP checks every
+ * frame from then on.
  * NETSTAT: a frame dropped here never reaches ProcessPacket, so get_rptr
  * counts it in rx_packets / rx_bytes as ProcessPacket would have
  * (eth_in.c:20-23) and core.c:774-775 counts the NULL in rx_errors: the three
@@ -135,6 +138,10 @@ struct gpu_private_context {
     int pipeline;                         /* serve aggregate k while k+1 is checked */
     int tx;                               /* tx checksums filled here        */
     long fail_after;                      /* MTCP_GPU_FAIL_AFTER: fault injection, -1 off */
+    long stall_after;                     /* MTCP_GPU_STALL_AFTER: fault injection, -1 off */
+    uint32_t stall_us;                    /* MTCP_GPU_STALL_US                */
+    uint32_t wait_us;                     /* MTCP_GPU_WAIT_TIMEOUT_MS, 0: no limit */
+    mtcp_gpu_ctx *hung;                   /* abandoned after a timed-out wait: never waited on */
     long launches;                        /* aggregates sent to the GPU       */
     struct gpu_ifq *ifq[MAX_DEVICES];     /* created at init (or first recv_pkts) */
     int ifq_failed[MAX_DEVICES];          /* no staging: this interface passes through */
@@ -150,6 +157,26 @@ static void gpu_ifq_wait(struct gpu_ifq *f)
     for (b = 0; b < 2; b++)
         if (f->rxq[b])
             (void)mtcp_gpu_rxq_wait(f->rxq[b], NULL);
+}
+
+/* A wait ran past MTCP_GPU_WAIT_TIMEOUT_MS: the GPU is not answering.
+ * Software checksums from now on, without waiting for it again: every
+ * aggregate still on it is abandoned (its frames are served unchecked and
+ * mTCP checks them), and its context and staging are never freed (freeing
+ * would wait for the device). */
+static void gpu_abandon(struct gpu_private_context *g)
+{
+    int i, b;
+    TRACE_ERROR("gpu_module: GPU did not answer within the wait limit; software checksums from now on\n");
+    g->hung = g->gpu;
+    g->gpu = NULL;
+    for (i = 0; i < MAX_DEVICES; i++)
+        if (g->ifq[i])
+            for (b = 0; b < 2; b++)
+                if (g->ifq[i]->rxq[b] && g->ifq[i]->launched[b]) {
+                    (void)mtcp_gpu_rxq_wait_for(g->ifq[i]->rxq[b], NULL, 1);
+                    g->ifq[i]->launched[b] = 0;
+                }
 }
 
 /* After any GPU error: let the queued work finish, then software checksums
@@ -281,6 +308,14 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
      * error would, so the fallback to mTCP's own checksums is exercised on a
      * healthy GPU (tests/test_dropin.py) */
     g->fail_after = getenv("MTCP_GPU_FAIL_AFTER") ? atol(getenv("MTCP_GPU_FAIL_AFTER")) : -1;
+    /* MTCP_GPU_STALL_AFTER=k, MTCP_GPU_STALL_US=u: the (k+1)-th aggregate
+     * waits u us on the GPU behind mtcp_gpu_debug_stall, so that the wait
+     * limit (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000; 0: none) and the
+     * fallback after it are exercised on a healthy GPU */
+    g->stall_after = getenv("MTCP_GPU_STALL_AFTER") ? atol(getenv("MTCP_GPU_STALL_AFTER")) : -1;
+    g->stall_us = getenv("MTCP_GPU_STALL_US") ? (uint32_t)atol(getenv("MTCP_GPU_STALL_US")) : 0;
+    g->wait_us = 1000u * (uint32_t)(getenv("MTCP_GPU_WAIT_TIMEOUT_MS") ? atol(getenv("MTCP_GPU_WAIT_TIMEOUT_MS"))
+                                                                     : 2000);
     if (g->tx && !gpu_tx_capable(gpu_inner_module)) {
         TRACE_ERROR("gpu_module: MTCP_GPU_TX=1 refused: the wrapped backend sends from get_wptr\n");
         g->tx = 0;
@@ -443,6 +478,8 @@ static uint32_t gather(struct mtcp_thread_context *ctx, struct gpu_ifq *f, int i
     f->count[a] = total;
     f->launched[a] = 0;
     if (total && g->gpu) {
+        if (g->launches == g->stall_after)
+            (void)mtcp_gpu_debug_stall(g->gpu, g->stall_us);
         if ((g->fail_after < 0 || g->launches < g->fail_after) &&
             mtcp_gpu_rxq_flush_async(q) == MTCP_GPU_OK) {
             f->launched[a] = 1;
@@ -460,11 +497,16 @@ static uint32_t gather(struct mtcp_thread_context *ctx, struct gpu_ifq *f, int i
 static void finish(struct gpu_private_context *g, struct gpu_ifq *f, int a)
 {
     uint32_t n_done = 0;
+    int rc;
     f->served_raw[a] = 1;
     if (!f->launched[a])
         return;
-    if (mtcp_gpu_rxq_wait(f->rxq[a], &n_done) == MTCP_GPU_OK && n_done == f->count[a])
+    f->launched[a] = 0;
+    rc = mtcp_gpu_rxq_wait_for(f->rxq[a], &n_done, g->wait_us);
+    if (rc == MTCP_GPU_OK && n_done == f->count[a])
         f->served_raw[a] = 0;
+    else if (rc == MTCP_GPU_ETIMEDOUT && g->gpu)
+        gpu_abandon(g);
     else if (g->gpu)
         gpu_fail(g);
 }
@@ -542,8 +584,10 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
         gpu_tx_flush(g, i);                          /* frames still recorded */
         free(g->txq[i]);
         if (g->ifq[i]) {
-            mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[0]);   /* NULL-safe; waits for its work */
-            mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[1]);
+            if (!g->hung) {                          /* a hung GPU's staging stays */
+                mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[0]);   /* NULL-safe; waits for its work */
+                mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[1]);
+            }
             free(g->ifq[i]);
         }
     }

@@ -43,13 +43,14 @@ BR_TCP_OK, BR_IP_SHORT, BR_IP_CSUM_BAD, BR_TCP_LEN_BAD, BR_TCP_CSUM_BAD = 0, 3, 
 NULL = 254
 
 
-def run_dropin(tmp_path, mode="observe", pipeline="1", fail_after=None):
+def run_dropin(tmp_path, mode="observe", pipeline="1", fail_after=None, inject=None):
     if not os.path.exists(EXE):
         pytest.fail("oracle/_ref/dropin_rx not built: `make -C oracle ref` (needs /root/reference)")
     out = tmp_path / f"dropin_{mode}_{pipeline}_{fail_after}.bin"
     env = dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX="0")
     if fail_after is not None:
         env["MTCP_GPU_FAIL_AFTER"] = str(fail_after)
+    env.update(inject or {})
     p = subprocess.run([EXE, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
                         str(out), mode], capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -149,17 +150,28 @@ def test_dropin_at_the_reference_call_sites(tmp_path, golden, mode, pipeline):
     assert padded.sum() >= 30 and (r["branch"][padded] == BR_TCP_OK).all()
 
 
+INJECT = {
+    "fail": {"MTCP_GPU_FAIL_AFTER": "1"},
+    # the second aggregate waits 400 ms behind mtcp_gpu_debug_stall; the
+    # module's wait gives up after 50 ms and abandons the GPU
+    "hang": {"MTCP_GPU_STALL_AFTER": "1", "MTCP_GPU_STALL_US": "400000", "MTCP_GPU_WAIT_TIMEOUT_MS": "50"},
+}
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("fault", ["fail", "hang"])
 @pytest.mark.parametrize("pipeline", ["1", "0"])
-def test_dropin_gpu_failure_falls_back_to_mtcp(tmp_path, golden, pipeline):
-    """A GPU error mid-stream (MTCP_GPU_FAIL_AFTER=1: the second aggregate's
-    launch fails): gpu_module serves the rest unchecked and answers dev_ioctl
-    -1, mTCP's own ip_fast_csum / TCPCalcChecksum take over (ip_in.c:29-31,
-    tcp_in.c:1160-1164), and the outcome of the whole run — every frame's
-    branch, return value and stream key, rx_packets / rx_bytes / rx_errors —
-    is still the --disable-hwcsum reference's (the frames of the failed part
-    are checked by the reference itself, ref-UB ones included)."""
-    stats, r = run_dropin(tmp_path, "observe", pipeline, fail_after=1)
+def test_dropin_gpu_failure_falls_back_to_mtcp(tmp_path, golden, pipeline, fault):
+    """A GPU error mid-stream (fail: MTCP_GPU_FAIL_AFTER=1, the second
+    aggregate's launch fails; hang: the second aggregate does not finish
+    within MTCP_GPU_WAIT_TIMEOUT_MS): gpu_module serves the rest unchecked
+    and answers dev_ioctl -1, mTCP's own ip_fast_csum / TCPCalcChecksum take
+    over (ip_in.c:29-31, tcp_in.c:1160-1164), and the outcome of the whole run
+    — every frame's branch, return value and stream key, rx_packets /
+    rx_bytes / rx_errors — is still the --disable-hwcsum reference's (the
+    frames of the failed part are checked by the reference itself, ref-UB
+    ones included)."""
+    stats, r = run_dropin(tmp_path, "observe", pipeline, inject=INJECT[fault])
     n = len(golden.desc)
     ub = golden.meta["ref_ub"] == 1
     ok = ~ub

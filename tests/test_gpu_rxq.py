@@ -69,3 +69,55 @@ def test_rxq_serves_the_oracle_verdicts(golden, mode):
                         assert ctypes.string_at(p, int(d["len"])) == frame.tobytes(), k
         finally:
             L.mtcp_gpu_rxq_destroy(q)
+
+
+@pytest.mark.gpu
+def test_rxq_wait_for_abandons_a_flush_that_does_not_finish(golden):
+    """mtcp_gpu_rxq_wait_for: a flush queued behind 300 ms of
+    mtcp_gpu_debug_stall is not in after 20 ms — MTCP_GPU_ETIMEDOUT, no
+    results served, the staged frames still served raw by rxq_frame, resets
+    and pushes taken again, further flushes refused (the abandoned one may
+    still write its results); with no limit, wait_for is rxq_wait."""
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    import time
+    from mtcp_amd import gpu
+    from mtcp_amd._lib import lib
+    L = lib()
+    ETIMEDOUT, EIO = -110, -5
+    buf, desc = golden.buf, golden.desc
+    base = buf.ctypes.data
+    part = desc[:256]
+    with gpu.Context(0) as ctx:
+        assert L.mtcp_gpu_debug_stall(ctx._h, 20 * 1000 * 1000) == EINVAL     # over the 10 s cap
+        q = ctypes.c_void_p()
+        assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 256, 256 * 2048) == 0
+        try:
+            for d in part:
+                assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
+            n_done = ctypes.c_uint32()
+            assert L.mtcp_gpu_rxq_flush_async(q) == 0
+            assert L.mtcp_gpu_rxq_wait_for(q, ctypes.byref(n_done), 0) == 0      # no limit: rxq_wait
+            assert n_done.value == len(part)
+            L.mtcp_gpu_rxq_reset(q)
+            for d in part:
+                assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
+            assert L.mtcp_gpu_debug_stall(ctx._h, 300 * 1000) == 0
+            t0 = time.monotonic()
+            assert L.mtcp_gpu_rxq_flush_async(q) == 0
+            assert L.mtcp_gpu_rxq_wait_for(q, ctypes.byref(n_done), 20 * 1000) == ETIMEDOUT
+            assert time.monotonic() - t0 < 0.25
+            assert n_done.value == 0
+            ln = ctypes.c_uint16()
+            assert L.mtcp_gpu_rxq_get(q, 0, ctypes.byref(ln), None) is None
+            p = L.mtcp_gpu_rxq_frame(q, 3, ctypes.byref(ln))
+            o, n = int(part[3]["offset"]), int(part[3]["len"])
+            assert ln.value == n and ctypes.string_at(p, n) == buf[o:o + n].tobytes()
+            L.mtcp_gpu_rxq_reset(q)
+            assert L.mtcp_gpu_rxq_pending(q) == 0
+            assert L.mtcp_gpu_rxq_push(q, base + int(part[0]["offset"]), int(part[0]["len"])) == 0
+            assert L.mtcp_gpu_rxq_flush_async(q) == EIO
+            assert L.mtcp_gpu_sync(ctx._h) == 0                  # the stall ends by itself
+            assert time.monotonic() - t0 >= 0.25
+        finally:
+            L.mtcp_gpu_rxq_destroy(q)
