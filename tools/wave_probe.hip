@@ -93,6 +93,11 @@ int main(int argc, char **argv) {
         printf("{\"L\": %u, \"n\": %u", L, n);
         const char *only = getenv("WP_ONLY");             // e.g. "full,phase1" (PMC runs)
         const int rounds = getenv("WP_ROUNDS") ? atoi(getenv("WP_ROUNDS")) : 5;
+        // WP_SYNC=1: wait for each launch before issuing the next, so that a
+        // rocprofv3 kernel trace sees every dispatch on an idle GPU (its
+        // begin->end is then the kernel's own, with no queueing behind the
+        // previous launch); the event figure then includes the host round trip
+        const bool sync_each = getenv("WP_SYNC") && atoi(getenv("WP_SYNC"));
         for (const V &v : vs) {
             if (only && !strstr(only, v.name)) continue;
             const uint32_t blocks = v.ppb ? (n + v.ppb - 1) / v.ppb : std::min<uint32_t>((n + 255) / 256, 512);
@@ -101,7 +106,10 @@ int main(int argc, char **argv) {
                 for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(v.fn, dim3(blocks), dim3(v.threads), 0, st, kp);
                 CK(hipEventRecord(a, st));
                 const int reps = rounds < 5 ? 2 : 100;
-                for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(v.fn, dim3(blocks), dim3(v.threads), 0, st, kp);
+                for (int i = 0; i < reps; ++i) {
+                    hipLaunchKernelGGL(v.fn, dim3(blocks), dim3(v.threads), 0, st, kp);
+                    if (sync_each) CK(hipStreamSynchronize(st));
+                }
                 CK(hipEventRecord(b, st));
                 CK(hipEventSynchronize(b));
                 float ms;
