@@ -96,6 +96,9 @@ def parse():
                     help="packets per GPU (default: the config's; tests use smaller batches)")
     ap.add_argument("--dump-records", default=None,
                     help="directory: each rank writes its result records there")
+    ap.add_argument("--numa", default="on", choices=["on", "off"],
+                    help="run each rank on the cpus local to its GPU (sysfs local_cpulist), so the "
+                         "host buffers of the CPU-baseline and PCIe-inclusive legs sit on its socket")
     ap.add_argument("--record", default="full", choices=["full", "compact"],
                     help="rx result record: the 40 B mtcp_gpu_result (default, the headline) or "
                          "the 16 B mtcp_gpu_result16 of a MTCP_GPU_F_COMPACT context")
@@ -127,6 +130,23 @@ def host_prefix(d_buf, desc, max_pkts=None, max_bytes=None):
     for o in range(0, end, step):
         host[o:o + step] = d_buf[o:min(o + step, end)].cpu().numpy()
     return host, desc[:n]
+
+
+def bind_to_device(device: int, mode: str) -> dict:
+    """Restrict this rank to the cpus local to its GPU before any host buffer
+    is touched (mode "on"), as mTCP keeps each thread and its memory on one
+    node (mtcp/src/cpu.c:54-79) and gpu_module.c picks the GPU on the
+    thread's node (gpu_topo.h).  Returns what was done, for the JSON line."""
+    from mtcp_amd import gpu
+    allowed = os.sched_getaffinity(0)
+    if mode != "on":
+        return {"binding": "off", "cpus": len(allowed)}
+    bdf, local = gpu.device_local_cpus(device)
+    use = local & allowed
+    if not use:
+        return {"binding": "none (sysfs gives no local cpus)", "gpu_pci": bdf, "cpus": len(allowed)}
+    os.sched_setaffinity(0, use)
+    return {"binding": "cpus local to the GPU", "gpu_pci": bdf, "cpus": len(use)}
 
 
 def lib_sha256() -> str:
@@ -515,6 +535,7 @@ def main():
     device = int(os.environ.get("MTCP_BENCH_DEVICE", local_rank))
     torch.cuda.set_device(device)
     from mtcp_amd import gpu   # loads libmtcp_gpu.so (raises if not built)
+    host_cpus = bind_to_device(device, args.numa)
 
     per_gpu = args.per_gpu or cfg["per_gpu"]
     n_total = per_gpu * world
@@ -669,6 +690,7 @@ def main():
                          "kernel": "mg::" + kernel, "avg_launch_ms": round(kern_ms_max, 5),
                          "algorithmic_bytes_per_launch": frame_bytes},
             "tcp_ok_fraction": round(ok_frac, 5),
+            "host_cpus": host_cpus,
         }
         line.update(extra)
         print(json.dumps(line), flush=True)

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 
 import numpy as np
 
@@ -247,6 +248,41 @@ class Context:
                                               max_out, ctypes.byref(found)),
               "mtcp_gpu_addr_pool_search")
         return out[:min(found.value, max_out)]
+
+
+def parse_cpulist(text: str) -> set[int]:
+    """The kernel's cpulist format ("0-3,8,10-11") as a set of cpu ids."""
+    cpus: set[int] = set()
+    for part in text.strip().split(","):
+        part = part.strip()
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def device_pci_bus_id(device: int) -> str:
+    """PCI address of `device` ("0000:a7:00.0"), lower case as sysfs names it."""
+    buf = ctypes.create_string_buffer(64)
+    check(lib().mtcp_gpu_device_pci_bus_id(device, buf, len(buf)), "mtcp_gpu_device_pci_bus_id")
+    return buf.value.decode().lower()
+
+
+def device_local_cpus(device: int, sysfs: str = "/sys") -> tuple[str, set[int]]:
+    """The cpus on `device`'s side of the host (sysfs
+    bus/pci/devices/<bdf>/local_cpulist): where a process that stages frames
+    for this GPU should run so that its host buffers (first-touched by it) sit
+    on the GPU's socket.  mTCP keeps each thread and its memory on one node
+    the same way (mtcp_core_affinitize, mtcp/src/cpu.c:54-79; DPDK queues on
+    the NIC's socket, dpdk_module.c:660-663; gpu_module.c picks the GPU by the
+    thread's node, gpu_topo.h).  An empty set when sysfs does not tell."""
+    bdf = device_pci_bus_id(device)
+    try:
+        with open(os.path.join(sysfs, "bus", "pci", "devices", bdf, "local_cpulist")) as f:
+            return bdf, parse_cpulist(f.read())
+    except (OSError, ValueError):
+        return bdf, set()
 
 
 def host_register(arr: np.ndarray) -> None:
