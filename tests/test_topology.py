@@ -84,3 +84,21 @@ def test_cpulist_parser_edges(topo_exe, tmp_path):
     assert [r[1] for r in rows] == [0, 3, 0, 3, 0, 0, 3, 3]
     assert [r[2] for r in rows] == [0, 0, 1, 1, 2, 3, 2, 3]
     assert [r[3] for r in rows] == [0 % 1] * 8
+
+
+def test_bench_host_binding_reads_local_cpulist(tmp_path, monkeypatch):
+    """bench.py --numa on: a rank runs on its GPU's local_cpulist (the same
+    sysfs file family gpu_topo.h reads), parsed in the kernel's list format."""
+    from mtcp_amd import gpu
+    assert gpu.parse_cpulist("64-127,192-255\n") == set(range(64, 128)) | set(range(192, 256))
+    assert gpu.parse_cpulist("0,2,4-5") == {0, 2, 4, 5}
+    assert gpu.parse_cpulist("") == set()
+    bdf = "0000:f4:00.0"
+    d = tmp_path / "bus" / "pci" / "devices" / bdf
+    d.mkdir(parents=True)
+    (d / "local_cpulist").write_text("8-11,40\n")
+    monkeypatch.setattr(gpu, "device_pci_bus_id", lambda device: bdf)
+    assert gpu.device_local_cpus(0, sysfs=str(tmp_path)) == (bdf, {8, 9, 10, 11, 40})
+    # a device sysfs does not describe: no binding
+    monkeypatch.setattr(gpu, "device_pci_bus_id", lambda device: "0000:01:00.0")
+    assert gpu.device_local_cpus(0, sysfs=str(tmp_path)) == ("0000:01:00.0", set())
