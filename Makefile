@@ -62,5 +62,9 @@ tools/occ_probe: tools/occ_probe.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
 tools/tx_probe: tools/tx_probe.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
 
+# bench.py's read-ceiling leg (measurement only, not the product)
+tools/libstream_ceiling.so: tools/stream_ceiling.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+
 tools/sector_probe: tools/sector_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $<

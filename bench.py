@@ -96,6 +96,9 @@ def parse():
                     help="packets per GPU (default: the config's; tests use smaller batches)")
     ap.add_argument("--dump-records", default=None,
                     help="directory: each rank writes its result records there")
+    ap.add_argument("--ceiling", default="on", choices=["on", "off"],
+                    help="time a plain read stream over the same frame buffer (tools/libstream_ceiling.so) "
+                         "and report the kernel against it (roofline.read_ceiling)")
     ap.add_argument("--numa", default="on", choices=["on", "off"],
                     help="run each rank on the cpus local to its GPU (sysfs local_cpulist), so the "
                          "host buffers of the CPU-baseline and PCIe-inclusive legs sit on its socket")
@@ -147,6 +150,26 @@ def bind_to_device(device: int, mode: str) -> dict:
         return {"binding": "none (sysfs gives no local cpus)", "gpu_pci": bdf, "cpus": len(allowed)}
     os.sched_setaffinity(0, use)
     return {"binding": "cpus local to the GPU", "gpu_pci": bdf, "cpus": len(use)}
+
+
+def read_ceiling(d_buf, nbytes, stream, reps=20):
+    """The box's read-only streaming ceiling on this rank's own frame buffer
+    (SURVEY §8(d)), measured now: the fastest of four plain non-temporal
+    grid-stride read streams over all `nbytes` (slot padding included),
+    tools/stream_ceiling.hip.  Measurement infrastructure, outside the timed
+    region; None when the probe library is not built."""
+    import ctypes
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "libstream_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    f = ctypes.CDLL(path).stream_ceiling_us
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
+                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    f.restype = ctypes.c_int
+    us, shape = ctypes.c_float(0.0), ctypes.c_int(0)
+    if f(d_buf.data_ptr(), nbytes, reps, stream.cuda_stream, ctypes.byref(us), ctypes.byref(shape)) != 0:
+        raise RuntimeError("stream_ceiling_us failed")
+    return float(us.value), int(shape.value)
 
 
 def lib_sha256() -> str:
@@ -611,6 +634,19 @@ def main():
         kern_ms_max = kern_ms
 
     kernel = ctx.last_kernel                 # the kernel the timed launches dispatched
+    ceiling = None
+    if args.ceiling == "on":
+        # every rank times its own GPU; the slowest GPU's stream is the ceiling
+        # the slowest rank's launches (kern_ms_max) are compared with
+        try:
+            ceiling = read_ceiling(d_buf, sh.nbytes, stream)
+        except Exception as exc:   # never costs the headline line
+            ceiling = repr(exc)
+        if world > 1:
+            t = torch.tensor([ceiling[0] if isinstance(ceiling, tuple) else -1.0], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if isinstance(ceiling, tuple):
+                ceiling = (float(t[0]), ceiling[1])
     # verdict summary of the last step (sanity: corruption rate ~1/1024 + 1/4096)
     recs = d_out.view(-1, rec_bytes)
     v_at, pl_at = (14, 8) if compact else (36, 32)   # verdict, payload_len (include/mtcp_gpu.h)
@@ -692,6 +728,18 @@ def main():
             "tcp_ok_fraction": round(ok_frac, 5),
             "host_cpus": host_cpus,
         }
+        if isinstance(ceiling, tuple):
+            cus, shape = ceiling
+            line["roofline"]["read_ceiling"] = {
+                "us": round(cus, 2), "GBs": round(sh.nbytes / cus / 1e3, 1),
+                "algorithmic_GBs": round(frame_bytes / cus / 1e3, 1),
+                "frac_of_peak": round(frame_bytes / cus / 1e3 / HBM_PEAK_GBS, 4),
+                "kernel_frac_of_ceiling": round(cus / (kern_ms_max * 1e3), 4),
+                "what": f"plain non-temporal read stream of the same {sh.nbytes} B frame buffer "
+                        f"(slot padding included), fastest of 4 shapes ({shape // 10} loads per lane, "
+                        f"{shape % 10} WG/CU), 20 launches, HIP events; tools/stream_ceiling.hip"}
+        elif ceiling is not None:
+            line["roofline"]["read_ceiling"] = {"error": ceiling}
         line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:

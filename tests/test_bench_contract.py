@@ -108,3 +108,15 @@ def test_self_launch_refuses_more_gpus_than_visible(tmp_path):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "64"],
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and "GPU(s) visible" in p.stderr
+
+
+def test_read_ceiling_probe_is_built_and_exported(bench, monkeypatch):
+    """bench.py's read-ceiling leg (roofline.read_ceiling) loads
+    tools/libstream_ceiling.so, which build() makes; on by default."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "libstream_ceiling.so")
+    assert os.path.exists(path), "run __graft_entry__.build()"
+    assert hasattr(ctypes.CDLL(path), "stream_ceiling_us")
+    monkeypatch.setattr("sys.argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.ceiling, a.numa) == ("on", "on")

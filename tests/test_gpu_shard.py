@@ -101,6 +101,9 @@ def test_bench_two_ranks_equal_one_launch(gpu, tmp_path, config, size, rss, per_
     line, metas, recs = _bench_ranks(tmp_path, config, per_gpu, launcher=launcher)
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["config"]["packets_total"] == 2 * per_gpu
+    # the measured read ceiling of the slowest rank's GPU, next to its kernel
+    rc = line["roofline"]["read_ceiling"]
+    assert rc["us"] > 0 and 0 < rc["kernel_frac_of_ceiling"] <= 1.2, rc
     first = 0
     for m, r in zip(metas, recs):
         assert m["first_index"] == first and m["count"] == len(r)

@@ -32,6 +32,28 @@ __global__ __launch_bounds__(256) void plain_stream_nt(mg::KParams kp) {
     if (acc == 0x12345678u) kp.out[0].saddr = acc;
 }
 
+// bench.py's read-ceiling stream (tools/stream_ceiling.hip) on the same
+// buffer: a generic pointer and __builtin_nontemporal_load on it, U loads
+// per lane in flight
+template <int U>
+__global__ __launch_bounds__(256) void plain_ceil(mg::KParams kp) {
+    const mg::v4u *p = reinterpret_cast<const mg::v4u *>(kp.buf);
+    const uint64_t n16 = kp.buf_len / 16;
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; i < n16; i += stride) {
+        mg::v4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = i + (uint64_t)u * 256;
+            v[u] = __builtin_nontemporal_load(p + (j < n16 ? j : n16 - 1));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = mg::halves4(v[u], acc);
+    }
+    if (acc == 0x9E3779B9u) kp.out[blockIdx.x].saddr = acc;
+}
+
 // Pure read-only stream over the same frame buffer (the measured ceiling on
 // THIS data): grid-stride dwordx4 + v_sad_u16, 4 loads in flight per lane.
 __global__ __launch_bounds__(256) void plain_stream(mg::KParams kp) {
@@ -668,6 +690,27 @@ int main(int argc, char **argv) {
             vs.push_back({"lad_B8_desc_st15_regs_coal16", ladder<8, true, 0, 15, false>, 2});
         }
         vs.push_back({"plain_stream_nt_cu2", plain_stream_nt, 2});
+        vs.push_back({"plain_ceil4_cu2", plain_ceil<4>, 2});
+        vs.push_back({"plain_ceil8_cu2", plain_ceil<8>, 2});
+        vs.push_back({"plain_ceil4_cu4", plain_ceil<4>, 4});
+        vs.push_back({"plain_ceil2_cu2", plain_ceil<2>, 2});
+        vs.push_back({"plain_ceil3_cu2", plain_ceil<3>, 2});
+        vs.push_back({"plain_ceil6_cu2", plain_ceil<6>, 2});
+        vs.push_back({"plain_ceil4_cu1", plain_ceil<4>, 1});
+        vs.push_back({"plain_ceil6_cu1", plain_ceil<6>, 1});
+        vs.push_back({"plain_ceil8_cu1", plain_ceil<8>, 1});
+        vs.push_back({"plain_ceil4_cu3", plain_ceil<4>, 3});
+        vs.push_back({"plain_ceil2_cu4", plain_ceil<2>, 4});
+        // waves per CU for the shipped C2 schedule: 6 (3 x 2, 2 x 3) and 4 (2 x 2)
+        vs.push_back({"wv_unrolled_wpb3_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 3>, 2, 3});
+        vs.push_back({"wv_unrolled_wpb2_cu3", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 2>, 3, 2});
+        vs.push_back({"wv_unrolled_wpb2_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 2>, 2, 2});
+        vs.push_back({"wv_abl1_nostore_wpb3_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0, 8, true, 6, false, false, 0, 3>, 2, 3});
+        vs.push_back({"u3_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 3>, 2});
+        vs.push_back({"u4_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 4>, 2});
+        vs.push_back({"u3_abl1_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0, 8, true, 3>, 2});
+        vs.push_back({"u4_abl1_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0, 8, true, 4>, 2});
+        vs.push_back({"wv_abl1_nostore_wpb2_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0, 8, true, 6, false, false, 0, 2>, 2, 2});
         vs.push_back({"runstream4_cu2", run_stream<4>, 2});
         vs.push_back({"runstream8_cu2", run_stream<8>, 2});
         vs.push_back({"runstream12_cu2", run_stream<12>, 2});
