@@ -712,9 +712,11 @@ struct Trip {
 // compact record has no 4-tuple to hash at the flush).
 // WPE: waves per SIMD the register allocation must allow (2: up to 256
 // VGPRs; 3: 168, a third workgroup per CU; tools/occ_probe.hip).
+// COOP: the workgroup loads its descriptors together (phase 0 below; the
+// unrolled schedule of the chunk modes); false: each lane its own (A/B).
 template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
           bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0,
-          int WPB = kWavesPerBlock, int XSKIP = 0, bool CMP = false, int WPE = 2>
+          int WPB = kWavesPerBlock, int XSKIP = 0, bool CMP = false, int WPE = 2, bool COOP = true>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE))) void rx_kernel(KParams kp) {
     uint64_t t_start = 0;
     if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
@@ -756,9 +758,37 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
     // ---------------- phase 0: descriptors (of the NEXT pass, prefetched) ---
     // The raw descriptor fields are loaded one pass ahead so that their
     // latency hides under the current pass's streaming.
+    // COOP (B == 8): the workgroup loads its descriptors together.  A lane's
+    // own descriptors lie 8 x 8 B per wave-run at a stride of 8 * nwaves
+    // packets, i.e. eight scattered 64 B pieces per wave and pass; the WPB
+    // waves of a workgroup own adjacent runs, so for each of the eight runs
+    // the workgroup's descriptors are one contiguous 8 * WPB-packet piece
+    // (256 B at WPB 4).  Each lane loads one entry of those pieces (one
+    // coalesced load per wave), and `exchange` hands every entry to the lane
+    // that owns its packet through LDS.  Scattered 64 B pieces cost the frame
+    // stream ~7 us of C2's 1.6 GB (tools/rx_variants lad_B8_desc 228.3 vs
+    // lad_B8_descwg 220.6 us, the arithmetic-address walk 221.8): each one
+    // opens a DRAM row for 64 B.  Chunk modes only: the pointer-burst RSS
+    // schedule has no registers for the entries in flight (it would spill),
+    // and pointer bursts are DPDK-sized, mostly taken by the small kernels.
+    constexpr bool kCoop = B == 8 && MODE != kRxPtrs && SCHED == 3 && COOP;
+    __shared__ uint64_t coop_a[kCoop ? 2 : 1][kCoop ? WPB * kWave : 1];   // double-buffered by pass
+    uint32_t coop_buf = 0;
+
+    // entry (run cj, packet cidx of the workgroup's piece) is this lane's to
+    // load; it belongs to lane cj * 8 + cidx % 8 of wave cidx / 8
+    const uint32_t cq = wib * kWave + lane, cj = cq / (8 * WPB), cidx = cq % (8 * WPB);
+    const uint32_t coop_off = cj * (nwaves * 8) + blockIdx.x * (8 * WPB) + cidx;   // from the pass base
+    const uint32_t coop_slot = (cidx / 8) * kWave + cj * 8 + (cidx % 8);
     uint64_t raw_a = 0;     // chunk mode: the 8-byte descriptor; ptrs mode: the pointer
     uint32_t raw_b = 0;     // ptrs mode: the length
+    uint64_t cv_a = 0;      // COOP: the entry this lane loaded for the workgroup
     auto fetch = [&](uint32_t g0) {
+        if constexpr (kCoop) {
+            const uint32_t kk = g0 + coop_off;
+            if (kk < kp.n) cv_a = *reinterpret_cast<const uint64_t *>(kp.desc + kk);
+            return;
+        }
         bool live;
         const uint32_t k = lane_pkt(g0, live);
         if (live) {
@@ -768,6 +798,21 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
             } else {
                 raw_a = *reinterpret_cast<const uint64_t *>(kp.desc + k);
             }
+        }
+    };
+    // COOP: the fetched entries to their owners (raw_a), once per
+    // pass before its first decode.  Every wave of the workgroup calls it the
+    // same number of times: before the pass loop, and where a next pass
+    // exists (has_next is the same for the whole grid).
+    // Two buffers, alternating: the entries of exchange k are read before
+    // the barrier of exchange k + 1, so buffer k & 1 is free again at
+    // exchange k + 2 and one barrier per pass suffices.
+    auto exchange = [&]() {
+        if constexpr (kCoop) {
+            coop_a[coop_buf][coop_slot] = cv_a;
+            __syncthreads();
+            raw_a = coop_a[coop_buf][wib * kWave + lane];
+            coop_buf ^= 1u;
         }
     };
     auto decode = [&](uint32_t g0) -> Frame {
@@ -1063,6 +1108,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
     };
 
     fetch(0);
+    exchange();
     v4u X[U], Y[U];
     Trip pre;                    // next pass's first trip, already issued into X
     bool have_pre = false;
@@ -1174,6 +1220,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
                 small_finish(b, vb);
             }
             if (has_next) {                           // the next pass's first large round
+                exchange();
                 const Frame fn = decode(g0 + pass_pkts);
                 prepare(fn, pre_nL, pre_nS);
                 if constexpr (SCHED == 6) {
@@ -1220,6 +1267,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
             });
             have_pre = false;
             if (has_next) {
+                exchange();
                 const Frame fn = decode(g0 + pass_pkts);
                 Trip n;
                 enter_round(fn, n, 0);
@@ -1256,6 +1304,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
             }
             if (has_next) {
                 Trip n;
+                exchange();
                 const Frame fn = decode(g0 + pass_pkts);
                 if (__ballot(fn.live) && first_trip(fn, n)) {
                     issue(n, X);

@@ -80,12 +80,14 @@ __global__ __launch_bounds__(256) void plain_stream(mg::KParams kp) {
 // Ladder from frame_pattern's walk to the rx kernel's phase 1 (C2 layout:
 // frames at a 1536 B stride), one feature at a time.
 //   B     packet<->lane interleave (64 = each wave walks 64 consecutive frames)
-//   DESC  addresses from the descriptors (load, bpermute, row broadcast)
+//   DESC  addresses from the descriptors (load, bpermute, row broadcast);
+//         2: the workgroup loads its 8 x 256 B of descriptors per pass
+//         together (contiguous pieces, through LDS) instead of 8 x 64 B per wave
 //   SUMS  0: per-lane accumulator; 1: row sums -> LDS (lane 15, branch)
 //   ST    per-pass stores: 0 none; 1 one dword per 40 B record; 2 one dword
 //         per packet into a dense array; 3 whole 40 B records (8 B pieces)
 //   DBUF  explicit double buffering of the rounds
-template <int B, bool DESC, int SUMS, int ST, bool DBUF>
+template <int B, int DESC, int SUMS, int ST, bool DBUF>
 __global__ __launch_bounds__(256) void ladder(mg::KParams kp) {
     using namespace mg;
     __shared__ uint32_t sums[4][64];
@@ -107,8 +109,20 @@ __global__ __launch_bounds__(256) void ladder(mg::KParams kp) {
         if constexpr (DESC) {
             uint64_t p = base;
             uint32_t nch = 0;
+            uint64_t raw = 0;
+            if constexpr (DESC == 2 && B == 8) {
+                __shared__ uint64_t dsc[4][64];
+                const uint32_t j = 2 * wib + (lane >> 5), idx = lane & 31;
+                const uint32_t kk = g0 + j * 8 * nw + 32 * blockIdx.x + idx;
+                const uint64_t v = kk < kp.n ? *reinterpret_cast<const uint64_t *>(kp.desc + kk) : 0ull;
+                __syncthreads();
+                dsc[idx >> 3][j * 8 + (idx & 7)] = v;
+                __syncthreads();
+                raw = dsc[wib][lane];
+            } else if (k < kp.n) {
+                raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
+            }
             if (k < kp.n) {
-                const uint64_t raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
                 p = base + ((uint64_t)(uint32_t)raw << kp.off_shift);
                 const uint32_t L = (uint32_t)(raw >> 32) & 0xFFFFu;
                 nch = (uint32_t)((((p + L + 15) & ~15ull) - (p & ~15ull)) >> 4);
@@ -681,6 +695,13 @@ int main(int argc, char **argv) {
         vs.push_back({"wpp_persist_cu8", wave_per_packet<true>, 8});
         if (strcmp(cfg, "c2") == 0) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
+            vs.push_back({"lad_B8_nodesc", ladder<8, false, 0, 0, false>, 2});
+            vs.push_back({"lad_B8_descwg", ladder<8, 2, 0, 0, false>, 2});
+            vs.push_back({"lad_B8_nodesc_dbuf", ladder<8, false, 0, 0, true>, 2});
+            vs.push_back({"lad_B8_desc_dbuf", ladder<8, true, 0, 0, true>, 2});
+            vs.push_back({"lad_B64_nodesc", ladder<64, false, 0, 0, false>, 2});
+            vs.push_back({"lad_B8_nodesc_cu1", ladder<8, false, 0, 0, false>, 1});
+            vs.push_back({"lad_B8_nodesc_cu3", ladder<8, false, 0, 0, false>, 3});
             vs.push_back({"lad_B8_desc_st2", ladder<8, true, 0, 2, false>, 2});
             vs.push_back({"lad_B8_desc_st3", ladder<8, true, 0, 3, false>, 2});
             vs.push_back({"lad_B8_desc_st4_nt", ladder<8, true, 0, 4, false>, 2});
@@ -706,6 +727,10 @@ int main(int argc, char **argv) {
         vs.push_back({"wv_unrolled_wpb2_cu3", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 2>, 3, 2});
         vs.push_back({"wv_unrolled_wpb2_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 2>, 2, 2});
         vs.push_back({"wv_abl1_nostore_wpb3_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0, 8, true, 6, false, false, 0, 3>, 2, 3});
+        vs.push_back({"nocoop_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 4, 0, false, 2, false>, 2});
+        vs.push_back({"b16_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 16>, 2});
+        vs.push_back({"b32_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 32>, 2});
+        vs.push_back({"nocoop_abl1_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0, 8, true, 6, false, false, 0, 4, 0, false, 2, false>, 2});
         vs.push_back({"u3_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 3>, 2});
         vs.push_back({"u4_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 4>, 2});
         vs.push_back({"u3_abl1_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0, 8, true, 3>, 2});
