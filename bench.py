@@ -154,7 +154,7 @@ def bind_to_device(device: int, mode: str) -> dict:
 
 def read_ceiling(d_buf, nbytes, stream, reps=20):
     """The box's read-only streaming ceiling on this rank's own frame buffer
-    (SURVEY §8(d)), measured now: the fastest of four plain non-temporal
+    (SURVEY §8(d)), measured now: the fastest of eight plain non-temporal
     grid-stride read streams over all `nbytes` (slot padding included),
     tools/stream_ceiling.hip.  Measurement infrastructure, outside the timed
     region; None when the probe library is not built."""
@@ -736,7 +736,7 @@ def main():
                 "frac_of_peak": round(frame_bytes / cus / 1e3 / HBM_PEAK_GBS, 4),
                 "kernel_frac_of_ceiling": round(cus / (kern_ms_max * 1e3), 4),
                 "what": f"plain non-temporal read stream of the same {sh.nbytes} B frame buffer "
-                        f"(slot padding included), fastest of 4 shapes ({shape // 10} loads per lane, "
+                        f"(slot padding included), fastest of 8 shapes ({shape // 10} loads per lane, "
                         f"{shape % 10} WG/CU), 20 launches, HIP events; tools/stream_ceiling.hip"}
         elif ceiling is not None:
             line["roofline"]["read_ceiling"] = {"error": ceiling}

@@ -7,9 +7,10 @@
 // A grid-stride walk over the whole buffer: each lane keeps U non-temporal
 // 16 B loads in flight (global_load_dwordx4 nt, as the rx kernels' frame
 // stream), v_sad_u16 folds them so the loads stay live, one word per
-// workgroup is written only if an impossible sum shows up.  Four shapes (U 4
-// or 8, 2 or 4 workgroups of 256 lanes per CU) are timed and the fastest is
-// the ceiling; every byte of the buffer, slot padding included, is read once.
+// workgroup is written only if an impossible sum shows up.  Eight shapes (U
+// 3, 4, 6 or 8, 2 or 4 workgroups of 256 lanes per CU) are timed and the
+// fastest is the ceiling (on C2's buffer U 3 at 2 per CU: 24 KB in flight per
+// CU); every byte of the buffer, slot padding included, is read once.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -64,15 +65,17 @@ int stream_ceiling_us(const void *buf, uint64_t bytes, int reps, void *stream, f
     const uint64_t n16 = bytes / 16;
     *best_us = 0.0f;
     *shape = 0;
-    for (int u : {4, 8}) {
+    for (int u : {3, 4, 6, 8}) {
         for (int per_cu : {2, 4}) {
             if (rc) break;
             const dim3 grid((unsigned)(per_cu * cus)), block(256);
             auto launch = [&] {
-                if (u == 4)
-                    hipLaunchKernelGGL(stream_read<4>, grid, block, 0, st, p, n16, sink);
-                else
-                    hipLaunchKernelGGL(stream_read<8>, grid, block, 0, st, p, n16, sink);
+                switch (u) {
+                case 3: hipLaunchKernelGGL(stream_read<3>, grid, block, 0, st, p, n16, sink); break;
+                case 4: hipLaunchKernelGGL(stream_read<4>, grid, block, 0, st, p, n16, sink); break;
+                case 6: hipLaunchKernelGGL(stream_read<6>, grid, block, 0, st, p, n16, sink); break;
+                default: hipLaunchKernelGGL(stream_read<8>, grid, block, 0, st, p, n16, sink); break;
+                }
             };
             for (int i = 0; i < 3; ++i) launch();
             if (hipEventRecord(a, st) != hipSuccess) { rc = -1; break; }
