@@ -730,6 +730,8 @@ int main(int argc, char **argv) {
         vs.push_back({"nocoop_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 6, false, false, 0, 4, 0, false, 2, false>, 2});
         vs.push_back({"b16_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 16>, 2});
         vs.push_back({"b32_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 32>, 2});
+        vs.push_back({"abl2_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 2, 0>, 2});
+        vs.push_back({"abl3_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 3, 0>, 2});
         vs.push_back({"nocoop_abl1_nostore_cu2", rx_kernel<kRxChunk, false, 3, false, 1, 0, 8, true, 6, false, false, 0, 4, 0, false, 2, false>, 2});
         vs.push_back({"u3_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 3>, 2});
         vs.push_back({"u4_unrolled_cu2", rx_kernel<kRxChunk, false, 3, false, 0, 8, 8, true, 4>, 2});
