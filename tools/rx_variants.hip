@@ -697,6 +697,7 @@ int main(int argc, char **argv) {
             vs.push_back({"lad_B8_desc", ladder<8, true, 0, 0, false>, 2});
             vs.push_back({"lad_B8_nodesc", ladder<8, false, 0, 0, false>, 2});
             vs.push_back({"lad_B8_descwg", ladder<8, 2, 0, 0, false>, 2});
+            vs.push_back({"lad_B8_descwg_sums", ladder<8, 2, 1, 0, false>, 2});
             vs.push_back({"lad_B8_nodesc_dbuf", ladder<8, false, 0, 0, true>, 2});
             vs.push_back({"lad_B8_desc_dbuf", ladder<8, true, 0, 0, true>, 2});
             vs.push_back({"lad_B64_nodesc", ladder<64, false, 0, 0, false>, 2});
