@@ -167,7 +167,12 @@ void launch_one(dim3 grid, dim3 block, hipStream_t st, const mg::KParams &kp) {
     // backwards so neighbouring frames' shared lines are read in one step
     // (C5: 4.768 -> 4.737 GB per launch = chunk + descriptors, no line twice)
     constexpr bool kRev = LALIGN && SCHED == mg::kSchedUnrolled;
-    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, SCHED, LALIGN, 0, 8, 8, kNT, 6, kRev, false,
+    // runs of 16 packets for the size-sorted chunk schedule (C3-shaped
+    // batches): its per-lane descriptors come in 128 B pieces instead of 64 B
+    // (tools/rx_variants c3: 133.8 vs 134.9 us, records identical); the
+    // unrolled schedule keeps 8 and loads them per workgroup (rx_kernel COOP)
+    constexpr int kB = SCHED == mg::kSchedSorted && !LALIGN && MODE == mg::kRxChunk ? 16 : 8;
+    hipLaunchKernelGGL((mg::rx_kernel<MODE, RSS, SCHED, LALIGN, 0, 8, kB, kNT, 6, kRev, false,
                                       prio_for<SCHED, LALIGN>(), mg::kWavesPerBlock, 0, CMP>),
                        grid, block, 0, st, kp);
 }

@@ -649,6 +649,8 @@ int main(int argc, char **argv) {
         vs.push_back({"runstream16skip_cu2", run_stream<16, true>, 2});
         vs.push_back({"runstream24skip_cu2", run_stream<24, true>, 2});
 
+        vs.push_back({"b16_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16>, 2});
+        vs.push_back({"b32_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 32>, 2});
         vs.push_back({"abl1_rss_sorted6_nostore_u8_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 8, true, 8>, 2});
         vs.push_back({"rss_sorted6_u8_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 8>, 2});
         vs.push_back({"rss_sorted6_u8_defer4_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 4, 8, true, 8>, 2});
