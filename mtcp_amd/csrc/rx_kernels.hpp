@@ -758,7 +758,8 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
     // ---------------- phase 0: descriptors (of the NEXT pass, prefetched) ---
     // The raw descriptor fields are loaded one pass ahead so that their
     // latency hides under the current pass's streaming.
-    // COOP (B == 8): the workgroup loads its descriptors together.  A lane's
+    // COOP (B == 8, the unrolled chunk schedule: C2, C4, C5 and the tx fill):
+    // the workgroup loads its descriptors together.  A lane's
     // own descriptors lie 8 x 8 B per wave-run at a stride of 8 * nwaves
     // packets, i.e. eight scattered 64 B pieces per wave and pass; the WPB
     // waves of a workgroup own adjacent runs, so for each of the eight runs
@@ -768,9 +769,10 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
     // that owns its packet through LDS.  Scattered 64 B pieces cost the frame
     // stream ~7 us of C2's 1.6 GB (tools/rx_variants lad_B8_desc 228.3 vs
     // lad_B8_descwg 220.6 us, the arithmetic-address walk 221.8): each one
-    // opens a DRAM row for 64 B.  Chunk modes only: the pointer-burst RSS
-    // schedule has no registers for the entries in flight (it would spill),
-    // and pointer bursts are DPDK-sized, mostly taken by the small kernels.
+    // opens a DRAM row for 64 B; the kernel gains 1.7-2.6 us.  Not for the
+    // size-sorted schedule (2.7-2.8 us slower: the barrier holds back its
+    // desynchronised waves; it takes runs of 16 instead, mtcp_gpu.hip), nor
+    // for pointer bursts (the RSS pointer schedule would spill).
     constexpr bool kCoop = B == 8 && MODE != kRxPtrs && SCHED == 3 && COOP;
     __shared__ uint64_t coop_a[kCoop ? 2 : 1][kCoop ? WPB * kWave : 1];   // double-buffered by pass
     uint32_t coop_buf = 0;
