@@ -361,12 +361,14 @@ def run_row(args):
         raise SystemExit("the f-row benches run on one GPU")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
+    host_cpus = bind_to_device(0, args.numa)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     want_cpu = args.cpu_baseline in ("on", "auto")
     line = {"metric": f"{args.config}: " + ROWS[args.config], "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "data": "synthetic", "config": {"workload": args.config}}
+            "vs_baseline": None, "data": "synthetic", "config": {"workload": args.config},
+            "host_cpus": host_cpus}
     n, seed = 1 << 20, 2
     if args.config in ("f1", "f3"):
         desc, nbytes = pktgen.layout(n, 1500, 6, seed)
