@@ -226,3 +226,29 @@ def test_host_pipeline_stage_growth_mid_call(gpu):
     assert_same(got, dev, "stage growth")
     idx = np.sort(np.random.default_rng(2).choice(n, size=1000, replace=False))
     assert_same(got[idx], oracle.rx_chunk(host, desc[idx], 6, oracle.rss_cfg(None, 3, 1)), "sample")
+
+
+@pytest.mark.parametrize("size,n", [(1500, (1 << 17) + 1000), (1500, (2 << 17) + 333), (2000, (1 << 17) + 77)])
+def test_unrolled_partial_last_pass(gpu, size, n):
+    """The unrolled schedule's workgroup descriptor loads (rx_kernel COOP: one
+    LDS exchange and barrier per pass) on batches whose last pass leaves whole
+    waves of a workgroup without a packet (they leave the pass loop while
+    their siblings finish): rx and the tx fill equal the oracle.  (1 << 17
+    packets fill one pass of the grid on a 256-CU MI355X: 512 workgroups x 4
+    waves x 64.)"""
+    seed = 41
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    want = oracle.rx_chunk(buf, desc, 6)
+    with gpu.Context(0) as ctx:
+        got = run_rx_dev(ctx, buf, desc, 6)
+        assert ctx.last_kernel.startswith("rx_kernel<unrolled"), ctx.last_kernel
+        assert_same(got, want, f"{size} B x {n}")
+        b = to_dev(buf)
+        ctx.tx_fill_dev(b, to_dev(desc), n, 6)
+        torch.cuda.synchronize()
+    fixed = buf.copy()
+    oracle.tx_fill(fixed, desc, 6)
+    assert not np.array_equal(fixed, buf)
+    assert np.array_equal(b.cpu().numpy(), fixed)
