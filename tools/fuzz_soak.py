@@ -44,6 +44,7 @@ def main():
     totals = {"batches": 0, "frames": 0, "rx_mismatch": 0, "ptrs_mismatch": 0,
               "compact_mismatch": 0, "tx_mismatch_bytes": 0}
     verdicts = np.zeros(12, np.int64)
+    kernels = {}                      # rx kernels the chunk launches dispatched, and how often
     t0 = time.time()
     for seed in range(first, first + count):
         aligned = bool(seed & 1)
@@ -64,6 +65,7 @@ def main():
             with gpu.Context(0, rss=True, rss_key=key, rss_queues=nq, rss_endian=bool(endian)) as ctx:
                 out = torch.zeros(n * 40, dtype=torch.uint8, device=DEV)
                 ctx.rx_chunk_dev(b, d, n, 0, out)
+                kernels[ctx.last_kernel] = kernels.get(ctx.last_kernel, 0) + 1
                 ptrs = torch.from_numpy(desc["offset"].astype(np.int64) + b.data_ptr()).to(DEV)
                 lens = torch.from_numpy(desc["len"].view(np.int16).copy()).to(DEV)
                 outp = torch.zeros(n * 40, dtype=torch.uint8, device=DEV)
@@ -92,7 +94,8 @@ def main():
                               **totals}), flush=True)
     print(json.dumps({"probe": "fuzz_soak", "first_seed": first, "seeds": count,
                       "frames_per_batch": frames, "scheds": SCHEDS, **totals,
-                      "verdicts_seen": verdicts.tolist(), "seconds": round(time.time() - t0, 1)}),
+                      "verdicts_seen": verdicts.tolist(), "kernels": kernels,
+                      "seconds": round(time.time() - t0, 1)}),
           flush=True)
     bad = sum(v for k, v in totals.items() if "mismatch" in k)
     return 1 if bad else 0
