@@ -32,8 +32,12 @@ clean:
 	rm -f $(LIB)
 	$(MAKE) -C oracle clean
 
+# the probe tools instantiate rx_kernel's profiling / timing-probe variants
+# (ABL, STAMP, XSKIP), which only a -DMTCP_GPU_TESTING build allows
+TOOLFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -w -DMTCP_GPU_TESTING
+
 tools/rx_variants: tools/rx_variants.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
+	$(HIPCC) $(TOOLFLAGS) -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
 
 tools/hbm_ceiling: tools/hbm_ceiling.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -w -o $@ $<
@@ -46,21 +50,33 @@ tools/pcie_probe: tools/pcie_probe.hip
 
 tools: tools/rx_variants tools/hbm_ceiling tools/store_probe tools/pcie_probe tools/wave_probe
 
+# The test-only library: mtcp_gpu_debug_stall (tests/c/mtcp_gpu_testing.h),
+# fault injection kept out of the product library
+TESTLIB := tests/c/libmtcp_gpu_testing.so
+$(TESTLIB): tests/c/gpu_testing.hip tests/c/mtcp_gpu_testing.h include/mtcp_gpu.h $(LIB)
+	$(HIPCC) $(HIPFLAGS) -Iinclude -shared -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib'
+
 # gpu_module.c driven by the RunMainLoop rx harness; the
-# mTCP types come from the test doubles in tests/c/mtcp_double.
-tests/c/rxloop: tests/c/rxloop.c mtcp_amd/io_module/gpu_module.c mtcp_amd/io_module/gpu_topo.h include/mtcp_gpu_rxq.h oracle/mtcp_oracle.c $(LIB)
-	gcc -std=gnu99 -O3 -Wall -pthread -Itests/c/mtcp_double -Iinclude -o $@ tests/c/rxloop.c \
-	    mtcp_amd/io_module/gpu_module.c oracle/mtcp_oracle.c -Lmtcp_amd/lib -lmtcp_gpu \
-	    -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib'
+# mTCP types come from the test doubles in tests/c/mtcp_double.  A test
+# build (-DMTCP_GPU_TESTING): the fault-injection variables are read.
+tests/c/rxloop: tests/c/rxloop.c mtcp_amd/io_module/gpu_module.c mtcp_amd/io_module/gpu_topo.h include/mtcp_gpu_rxq.h oracle/mtcp_oracle.c $(LIB) $(TESTLIB)
+	gcc -std=gnu99 -O3 -Wall -pthread -DMTCP_GPU_TESTING -Itests/c/mtcp_double -Itests/c -Iinclude -o $@ tests/c/rxloop.c \
+	    mtcp_amd/io_module/gpu_module.c oracle/mtcp_oracle.c -Lmtcp_amd/lib -Ltests/c -lmtcp_gpu -lmtcp_gpu_testing -ldl \
+	    -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib' -Wl,-rpath,'$$ORIGIN'
+
+# the admission / limit logic of gpu_module.c, unit-tested on the CPU
+tests/c/admit_test: tests/c/admit_test.c mtcp_amd/io_module/gpu_module.c $(LIB)
+	gcc -std=gnu99 -O1 -Wall -pthread -Itests/c/mtcp_double -Iinclude -o $@ tests/c/admit_test.c \
+	    oracle/mtcp_oracle.c -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib'
 
 tools/wave_probe: tools/wave_probe.hip mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/rx_kernels.hpp $(LIB)
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
+	$(HIPCC) $(TOOLFLAGS) -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
 
 tools/occ_probe: tools/occ_probe.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
+	$(HIPCC) $(TOOLFLAGS) -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
 
 tools/tx_probe: tools/tx_probe.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -w -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
+	$(HIPCC) $(TOOLFLAGS) -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
 
 # bench.py's read-ceiling leg (measurement only, not the product)
 tools/libstream_ceiling.so: tools/stream_ceiling.hip

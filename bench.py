@@ -7,7 +7,11 @@ config asks for it) over one resident batch of synthetic frames.  Frames are
 generated on the GPU (include/mtcp_gpu_pktgen.h) and stay in HBM; results
 (40 B per packet) are written to HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1..c5|f1|f3|f4] [--strong]
+
+Without --config the workload is BASELINE.json's config for that N: C2
+(1 M x 1500 B) on one GPU, C4 (2 M x 1500 B per GPU, 16 M at N = 8) on
+N > 1; config.workload names the total.
 
 MTCP_BENCH_DEVICE=d in the environment puts every rank on device d (a
 rehearsal of the N > 1 path on a one-GPU box; the timings then mean
@@ -15,17 +19,20 @@ nothing), and --dump-records DIR writes each rank's result records after the
 timed steps (tests/test_gpu_shard.py compares them with one launch over the
 whole batch).
 
-Multi-GPU: one process per GPU, weak scaling — each
-rank processes its own contiguous shard of one global batch (batch split, no
-collective on the data path; gloo carries only the barrier and the max of the
-per-rank times).  Rank 0 prints ONE JSON line.  Under torch.distributed.run
-(WORLD_SIZE set) each process is one rank; `python bench.py --gpus N` with no
-launcher starts its N ranks itself (self_launch) and forwards that line.
+Multi-GPU: one process per GPU, weak scaling (--strong: the whole batch
+split N ways) — each rank processes its own contiguous shard of one global
+batch (batch split, no collective on the data path; gloo carries only the
+barrier and the max of the per-rank times).  Rank 0 prints ONE JSON line.
+Under torch.distributed.run (WORLD_SIZE set) each process is one rank;
+`python bench.py --gpus N` with no launcher starts its N ranks itself
+(self_launch) and forwards that line.
 
-The CPU baseline (rank 0, N=1 only) times the reference's own rx code
-(oracle/_ref/libref_rx.so, compiled from /root/reference) or, where that
-was not built, the oracle's C restatement, on a bounded sample of the same
-frames copied to host memory.
+The CPU baseline times the reference's own rx code (oracle/_ref/libref_rx.so,
+compiled from /root/reference) or, where that was not built, the oracle's C
+restatement, on a bounded sample of the same frames copied to host memory:
+at N = 1 on rank 0 with 1 core and with its GPU-local share; at N > 1 on
+every rank at once, each on its own disjoint GPU-local cores, reported per
+rank and as the host aggregate.
 """
 from __future__ import annotations
 
@@ -55,11 +62,56 @@ CONFIGS = {
                desc="1 M x 1500 B (MTU) packets, IP+TCP checksum + header parse"),
     "c3": dict(size="bimodal", per_gpu=1 << 20, rss=True, seed=3,
                desc="1 M packets bimodal 64 B / 1500 B + RSS Toeplitz hash"),
-    "c4": dict(size=1500, per_gpu=1 << 21, rss=False, seed=4,
+    "c4": dict(size=1500, per_gpu=1 << 21, total=1 << 24, rss=False, seed=4,
                desc="16 M x 1500 B packets sharded across 8 MI355X (2 M per GPU)"),
-    "c5": dict(size=9000, per_gpu=1 << 19, rss=False, seed=5,
+    "c5": dict(size=9000, per_gpu=1 << 19, total=1 << 22, rss=False, seed=5,
                desc="4 M x 9000 B jumbo frames (512 K per GPU), checksum + parse"),
 }
+
+# what each config computes, for config.workload (the sizes come from the run)
+WHAT = {"c1": "TCP segments, checksum + parse", "c2": "packets, IP+TCP checksum + header parse",
+        "c3": "packets, IP+TCP checksum + header parse + RSS Toeplitz hash",
+        "c4": "packets, IP+TCP checksum + header parse",
+        "c5": "jumbo frames, checksum + parse"}
+
+
+def default_config(gpus: int) -> str:
+    """The workload of `bench.py --gpus N` without --config: BASELINE.json's
+    configs[1] (C2, 1 M x 1500 B, the metric's own single-GPU config) at
+    N = 1; its multi-GPU config C4 (2 M x 1500 B per GPU, 16 M at N = 8)
+    at N > 1."""
+    return "c2" if gpus <= 1 else "c4"
+
+
+def _count(n: int) -> str:
+    if n % (1 << 20) == 0:
+        return f"{n >> 20} M"
+    if n % (1 << 10) == 0:
+        return f"{n >> 10} K"
+    return str(n)
+
+
+def workload(config: str, world: int, per_gpu_override=None, strong: bool = False) -> dict:
+    """Packets per rank and in total, and the scaling, of one run.  Weak (the
+    default): every rank processes the config's per-GPU batch, so C4 at N
+    GPUs is N x 2 M (16 M at N = 8).  --strong: the config's whole batch
+    (C4 16 M, C5 4 M; C1-C3 their one-GPU batch) split N ways, as SURVEY
+    §8(d) phrases C4.  --per-gpu overrides the per-rank count (tests)."""
+    cfg = CONFIGS[config]
+    size = cfg["size"]
+    if per_gpu_override:
+        per_gpu, scaling = per_gpu_override, "weak"
+        total = per_gpu * world
+    elif strong:
+        total, scaling = cfg.get("total", cfg["per_gpu"]), "strong"
+        per_gpu = total // world
+    else:
+        per_gpu, scaling = cfg["per_gpu"], "weak"
+        total = per_gpu * world
+    sz = "bimodal 64 B / 1500 B" if size == "bimodal" else f"{size} B"
+    desc = (f"{config}: {_count(total)} x {sz} {WHAT[config]}, "
+            + (f"{_count(per_gpu)} per GPU x {world} MI355X (batch split)" if world > 1 else "1 MI355X"))
+    return {"config": config, "per_gpu": per_gpu, "total": total, "scaling": scaling, "desc": desc}
 
 
 # SURVEY §8(f) rows beside the rx path, each measured on one GPU (not the
@@ -78,7 +130,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + sorted(ROWS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS) + sorted(ROWS),
+                    help="default: c2 at --gpus 1, c4 (2 M x 1500 B per GPU) at --gpus N > 1")
+    ap.add_argument("--strong", action="store_true",
+                    help="split the config's whole batch N ways (C4: 16 M) instead of N x its per-GPU batch")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
                     help="packets in the CPU sample (default: the whole 1-GPU batch, "
@@ -105,7 +160,10 @@ def parse():
     ap.add_argument("--record", default="full", choices=["full", "compact"],
                     help="rx result record: the 40 B mtcp_gpu_result (default, the headline) or "
                          "the 16 B mtcp_gpu_result16 of a MTCP_GPU_F_COMPACT context")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config is None:
+        a.config = default_config(a.gpus)
+    return a
 
 
 def cpu_model() -> str:
@@ -135,21 +193,36 @@ def host_prefix(d_buf, desc, max_pkts=None, max_bytes=None):
     return host, desc[:n]
 
 
-def bind_to_device(device: int, mode: str) -> dict:
+def bind_to_device(device: int, mode: str, world: int = 1, rank: int = 0) -> dict:
     """Restrict this rank to the cpus local to its GPU before any host buffer
     is touched (mode "on"), as mTCP keeps each thread and its memory on one
     node (mtcp/src/cpu.c:54-79) and gpu_module.c picks the GPU on the
-    thread's node (gpu_topo.h).  Returns what was done, for the JSON line."""
+    thread's node (gpu_topo.h).  With N > 1 ranks, the ranks whose GPUs
+    share a node split its cores (whole physical cores, shard.split_cpus),
+    so that their concurrent CPU baselines run on disjoint cores.  Returns
+    what was done, for the JSON line."""
     from mtcp_amd import gpu
     allowed = os.sched_getaffinity(0)
-    if mode != "on":
-        return {"binding": "off", "cpus": len(allowed)}
-    bdf, local = gpu.device_local_cpus(device)
-    use = local & allowed
-    if not use:
-        return {"binding": "none (sysfs gives no local cpus)", "gpu_pci": bdf, "cpus": len(allowed)}
-    os.sched_setaffinity(0, use)
-    return {"binding": "cpus local to the GPU", "gpu_pci": bdf, "cpus": len(use)}
+    info = {"binding": "off"}
+    use = set(allowed)
+    bdf = None
+    if mode == "on":
+        bdf, local = gpu.device_local_cpus(device)
+        info = {"binding": "cpus local to the GPU", "gpu_pci": bdf}
+        if local & allowed:
+            use = local & allowed
+        else:
+            info["binding"] = "none (sysfs gives no local cpus)"
+    if world > 1:
+        sets = [None] * world
+        dist.all_gather_object(sets, sorted(use))
+        peers = [r for r in range(world) if sets[r] == sets[rank]]
+        use = shard.split_cpus(use, peers.index(rank), len(peers))
+        info["shared_with_ranks"] = peers
+    if use != allowed:
+        os.sched_setaffinity(0, use)
+    info["cpus"] = len(use)
+    return info
 
 
 def read_ceiling(d_buf, nbytes, stream, reps=20):
@@ -249,6 +322,55 @@ def cpu_baseline(host_buf, desc, cfg, sample_n):
         "per_core_count": per_core(runs),
         "cpu_model": cpu_model(),
         **extra,
+    }
+
+
+def cpu_baseline_ranks(host_buf, desc, cfg, sample_n, world, rank):
+    """N > 1: the reference's rx code on every rank's own GPU-local core share
+    at the same time (bind_to_device gave the ranks disjoint cores), each
+    over the first frames of its own shard — the host doing the same job on
+    the cores that feed these GPUs, as mTCP runs one share-nothing thread
+    per core and queue (mtcp/src/core.c:1195-1213, dpdk_module.c:644-676).
+    The ranks start together after a barrier; each reports its best of 5
+    after a warm-up.  Rank 0 returns the per-rank figures and the host
+    aggregate (every rank's sample bytes / the slowest rank's time); the
+    other ranks return None."""
+    import oracle   # test infrastructure: the baseline leg only
+    n = min(sample_n, len(desc))
+    d = desc[:n].copy()
+    end = (int(d["offset"][-1]) << 6) + ((int(d["len"][-1]) + 63) & ~63)
+    buf = np.ascontiguousarray(host_buf[:end])
+    nbytes = int(d["len"].astype(np.int64).sum())
+    cores = cpu_share()
+    kind = "reference" if oracle.ref_available() else "port"
+    dist.barrier()
+    if kind == "reference":
+        best = oracle.ref_bench_rx(buf, d, 6, cfg["rss"], cores, 5)
+    else:
+        best = oracle.bench_rx(buf, d, 6, oracle.rss_cfg(None, 8, 1) if cfg["rss"] else None, cores, 5)
+    mine = torch.tensor([nbytes, n, best, cores, float(ord(kind[0]))], dtype=torch.float64)
+    rows = [torch.zeros(5, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(rows, mine)
+    if rank != 0:
+        return None
+    rows = [r.tolist() for r in rows]
+    kinds = {"reference" if int(r[4]) == ord("r") else "port" for r in rows}
+    total_bytes = sum(r[0] for r in rows)
+    total_pkts = sum(r[1] for r in rows)
+    slowest = max(r[2] for r in rows)
+    return {
+        "value": round(total_bytes / slowest / 1e9, 3), "unit": "GB/s",
+        "cores": int(sum(r[3] for r in rows)), "kind": kind if len(kinds) == 1 else "mixed",
+        "mpkt_per_s": round(total_pkts / slowest / 1e6, 3),
+        "scope": f"host aggregate: {world} ranks at once, each on its own GPU-local cores",
+        "per_rank": [{"rank": i, "cores": int(r[3]), "GB/s": round(r[0] / r[2] / 1e9, 3),
+                      "Mpkt/s": round(r[1] / r[2] / 1e6, 3), "seconds": round(r[2], 6)}
+                     for i, r in enumerate(rows)],
+        "sample": f"each rank the first {n} packets of its own shard, best of 5 after warm-up, "
+                  f"one pinned thread per core on contiguous pieces, all ranks started together "
+                  f"({'mtcp/src eth_in/ip_in/tcp_in/tcp_util compiled from /root/reference' if kind == 'reference' else 'oracle/mtcp_oracle.c restatement'}, gcc -O3); "
+                  f"aggregate = all ranks' sample bytes / the slowest rank's time",
+        "cpu_model": cpu_model(),
     }
 
 
@@ -560,10 +682,10 @@ def main():
     device = int(os.environ.get("MTCP_BENCH_DEVICE", local_rank))
     torch.cuda.set_device(device)
     from mtcp_amd import gpu   # loads libmtcp_gpu.so (raises if not built)
-    host_cpus = bind_to_device(device, args.numa)
+    host_cpus = bind_to_device(device, args.numa, world, rank)
 
-    per_gpu = args.per_gpu or cfg["per_gpu"]
-    n_total = per_gpu * world
+    wl = workload(args.config, world, args.per_gpu, args.strong)
+    per_gpu, n_total = wl["per_gpu"], wl["total"]
     sh = shard.make_shard(n_total, cfg["size"], rank, world, cfg["seed"])
     dev = torch.device("cuda", device)
     # a dedicated (non-null) stream: the kernel and the timing events share it
@@ -676,14 +798,21 @@ def main():
     payload_gbs = total_payload * args.steps / elapsed / 1e9
 
     extra = {}
-    want_cpu = rank == 0 and world == 1 and args.cpu_baseline in ("on", "auto")
+    # the CPU baseline at every N: rank 0 alone at N = 1 (1 core and its
+    # share), every rank at once on its own cores at N > 1 (a collective step)
+    want_cpu = args.cpu_baseline in ("on", "auto")
     want_pcie = args.pcie in ("on", "auto")     # every rank: a collective step when N > 1
     if want_cpu:
         host, hdesc = host_prefix(d_buf, sh.desc, max_pkts=args.cpu_sample)
-        try:
-            extra["cpu_baseline"] = cpu_baseline(host, hdesc, cfg, args.cpu_sample)
-        except Exception as exc:   # report, never fake
-            extra["cpu_baseline"] = {"value": None, "error": repr(exc)}
+        if world == 1:
+            try:
+                extra["cpu_baseline"] = cpu_baseline(host, hdesc, cfg, args.cpu_sample)
+            except Exception as exc:   # report, never fake
+                extra["cpu_baseline"] = {"value": None, "error": repr(exc)}
+        else:
+            cb = cpu_baseline_ranks(host, hdesc, cfg, args.cpu_sample, world, rank)
+            if rank == 0:
+                extra["cpu_baseline"] = cb
         del host
     if rank == 0 and world == 1 and args.small_batch != "off":
         try:
@@ -714,10 +843,10 @@ def main():
         line = {
             "metric": METRIC, "value": round(gbs, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "higher_is_better": True, "scaling": wl["scaling"], "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (GPU splitmix64 frames, include/mtcp_gpu_pktgen.h)",
             "gpkt_per_s": round(gpps, 4), "payload_gbs": round(payload_gbs, 2),
-            "config": {"workload": args.config + ": " + cfg["desc"], "packets_per_gpu": per_gpu,
+            "config": {"workload": wl["desc"], "packets_per_gpu": per_gpu,
                        "packets_total": total_pkts, "frame_bytes_total": total_bytes,
                        "rss": cfg["rss"], "parallelism": f"batch split x{world} (no collective)",
                        "launch": "hip_graph" if use_graph else "direct",

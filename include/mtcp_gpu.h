@@ -70,7 +70,8 @@
 extern "C" {
 #endif
 
-#define MTCP_GPU_ABI_VERSION 2   /* 2: MTCP_GPU_F_COMPACT, mtcp_gpu_result16 */
+#define MTCP_GPU_ABI_VERSION 3   /* 2: MTCP_GPU_F_COMPACT, mtcp_gpu_result16;
+                                    3: mtcp_gpu_rxq_get16, mtcp_gpu_debug_stall moved to the test library */
 
 /* ---- error codes (negative returns) ----------------------------------- */
 #define MTCP_GPU_OK        0
@@ -388,10 +389,8 @@ int mtcp_gpu_host_unregister(void *ptr);
 /* Synchronise the context's stream. */
 int mtcp_gpu_sync(mtcp_gpu_ctx *ctx);
 
-/* Fault injection for tests of a caller's hang handling: queue a kernel on
- * the context's stream that keeps it busy for `us` microseconds (at most
- * 10 s), so that work queued behind it completes that much later. */
-int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us);
+/* (The fault-injection entry point the hang tests use, mtcp_gpu_debug_stall,
+ * is not part of this library: tests/c/mtcp_gpu_testing.h.) */
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,15 @@ typedef struct mtcp_gpu_rxq mtcp_gpu_rxq;
 /* Staging for up to max_pkts frames / max_bytes (64 B aligned) bytes. */
 int  mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts,
                          uint64_t max_bytes);
+
+/* Free the rxq.  A flush still in flight is waited for.  After
+ * mtcp_gpu_rxq_wait_for gave up on a flush (MTCP_GPU_ETIMEDOUT), that flush
+ * may still copy into the staging and results: destroy then waits for it at
+ * most MTCP_GPU_RXQ_DESTROY_WAIT_US more, and if it still has not finished,
+ * the rxq's pinned and device buffers are left allocated (leaked, never
+ * touched again) instead of freed under the DMA, and destroy returns without
+ * blocking on the device.  Safe to call straight after ETIMEDOUT. */
+#define MTCP_GPU_RXQ_DESTROY_WAIT_US 100000u
 void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q);
 
 /* Copy one received frame (get_rptr's pointer and *len) into staging. */
@@ -83,13 +92,19 @@ int  mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n);
 int  mtcp_gpu_rxq_wait_for(mtcp_gpu_rxq *q, uint32_t *n, uint32_t timeout_us);
 
 /* get_rptr for flushed frame i: the staged frame and its length, or NULL for
- * the verdicts listed above.  *res (may be NULL) receives the frame's result
- * record: a mtcp_gpu_result, or — when the rxq's context was opened with
- * MTCP_GPU_F_COMPACT (mtcp_gpu_record_size 16) — a mtcp_gpu_result16, cast.
+ * the verdicts listed above.  *res (may be NULL) receives the frame's 40 B
+ * result record; on an rxq of a MTCP_GPU_F_COMPACT context (16 B records,
+ * mtcp_gpu_record_size 16) *res is set to NULL — use mtcp_gpu_rxq_get16.
  * A compact context moves 16 B per frame back instead of 40 (gpu_module.c's
  * rxqs read the verdict only). */
 uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
                           const mtcp_gpu_result **res);
+
+/* mtcp_gpu_rxq_get for the rxq of a compact context: *res16 (may be NULL)
+ * receives the frame's mtcp_gpu_result16; on a 40 B context *res16 is set
+ * to NULL (use mtcp_gpu_rxq_get).  The frame pointer is rxq_get's. */
+uint8_t *mtcp_gpu_rxq_get16(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
+                            const mtcp_gpu_result16 **res16);
 
 /* The staged copy of frame i (flushed or not), without a verdict: what a
  * backend serves when the GPU is unavailable and dev_ioctl answers -1. */

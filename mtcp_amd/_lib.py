@@ -20,11 +20,10 @@ EXPORTS = (
     "mtcp_gpu_rx_ptrs_dev", "mtcp_gpu_rx_chunk", "mtcp_gpu_rx_ptrs", "mtcp_gpu_tx_fill_dev",
     "mtcp_gpu_tx_fill", "mtcp_gpu_rx_chunk_flow_dev", "mtcp_gpu_rx_ptrs_flow_dev",
     "mtcp_gpu_tx_fill_ptrs_dev", "mtcp_gpu_tx_fill_ptrs", "mtcp_gpu_host_register", "mtcp_gpu_host_unregister", "mtcp_gpu_sync",
-    "mtcp_gpu_debug_stall",
     "mtcp_gpu_flow_hash_dev", "mtcp_gpu_flow_hash", "mtcp_gpu_rss_queue_map_dev",
     "mtcp_gpu_addr_pool_search", "mtcp_gpu_pktgen_dev",
     "mtcp_gpu_rxq_create", "mtcp_gpu_rxq_destroy", "mtcp_gpu_rxq_push", "mtcp_gpu_rxq_push_chunk",
-    "mtcp_gpu_rxq_pending", "mtcp_gpu_rxq_flush", "mtcp_gpu_rxq_flush_async", "mtcp_gpu_rxq_wait", "mtcp_gpu_rxq_wait_for", "mtcp_gpu_rxq_get", "mtcp_gpu_rxq_frame", "mtcp_gpu_rxq_reset",
+    "mtcp_gpu_rxq_pending", "mtcp_gpu_rxq_flush", "mtcp_gpu_rxq_flush_async", "mtcp_gpu_rxq_wait", "mtcp_gpu_rxq_wait_for", "mtcp_gpu_rxq_get", "mtcp_gpu_rxq_get16", "mtcp_gpu_rxq_frame", "mtcp_gpu_rxq_reset",
 )
 
 _lib = None
@@ -61,7 +60,6 @@ def lib() -> ctypes.CDLL:
         "mtcp_gpu_record_size": ([vp], u32),
         "mtcp_gpu_last_kernel": ([vp], ctypes.c_char_p),
         "mtcp_gpu_sync": ([vp], i32),
-        "mtcp_gpu_debug_stall": ([vp, u32], i32),
         "mtcp_gpu_rx_chunk_dev": ([vp, vp, u64, vp, u32, u32, vp, vp], i32),
         "mtcp_gpu_rx_ptrs_dev": ([vp, vp, u16p, u32, vp, vp], i32),
         "mtcp_gpu_rx_chunk": ([vp, vp, u64, vp, u32, u32, vp], i32),
@@ -91,6 +89,7 @@ def lib() -> ctypes.CDLL:
         "mtcp_gpu_rxq_wait": ([vp, ctypes.POINTER(u32)], i32),
         "mtcp_gpu_rxq_wait_for": ([vp, ctypes.POINTER(u32), u32], i32),
         "mtcp_gpu_rxq_get": ([vp, u32, ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(vp)], vp),
+        "mtcp_gpu_rxq_get16": ([vp, u32, ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(vp)], vp),
         "mtcp_gpu_rxq_frame": ([vp, u32, ctypes.POINTER(ctypes.c_uint16)], vp),
         "mtcp_gpu_rxq_reset": ([vp], None),
     }

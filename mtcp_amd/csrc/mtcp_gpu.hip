@@ -58,13 +58,6 @@ struct mtcp_gpu_ctx {
 
 namespace {
 
-// mtcp_gpu_debug_stall: one wave that returns `ticks` of the 100 MHz
-// s_memrealtime clock after it started (it reads the clock, writes nothing)
-__global__ __launch_bounds__(64) void stall_kernel(uint64_t ticks) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
-}
-
 // MTCP_GPU_DEBUG=1 in the environment: report every failing HIP call.
 bool hip_ok(hipError_t e, const char *what) {
     if (e == hipSuccess) return true;
@@ -551,14 +544,6 @@ int mtcp_gpu_sync(mtcp_gpu_ctx *ctx) {
     if (!ctx) return MTCP_GPU_EINVAL;
     DeviceGuard dg(ctx->device);
     return HIP_OK(hipStreamSynchronize(ctx->stream)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
-}
-
-int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us) {
-    if (!ctx || us > 10u * 1000 * 1000) return MTCP_GPU_EINVAL;
-    DeviceGuard dg(ctx->device);
-    if (!dg.ok) return MTCP_GPU_ENODEV;
-    hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, ctx->stream, (uint64_t)us * 100);
-    return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
 
 int mtcp_gpu_rx_chunk_flow_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,

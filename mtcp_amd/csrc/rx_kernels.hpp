@@ -718,6 +718,12 @@ template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int D
           bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0,
           int WPB = kWavesPerBlock, int XSKIP = 0, bool CMP = false, int WPE = 2, bool COOP = true>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE))) void rx_kernel(KParams kp) {
+#ifndef MTCP_GPU_TESTING
+    // the product library instantiates no profiling or timing-probe variant
+    // (XSKIP's records are wrong by design): those exist for tools/ only
+    static_assert(ABL == 0 && !STAMP && XSKIP == 0,
+                  "rx_kernel's ABL / STAMP / XSKIP variants need a -DMTCP_GPU_TESTING build (tools/)");
+#endif
     uint64_t t_start = 0;
     if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
     if constexpr ((PRIO & 3) > 0) {

@@ -81,6 +81,9 @@ __device__ __forceinline__ uint32_t toeplitz_wave(const uint32_t (&kw)[4], uint3
 // WPB: waves (= packets) per workgroup.
 template <int MODE, bool RSS, int ABL = 0, int SEG = 1, int NL = kWaveLoads, int WPB = kWavesPerBlock>
 __global__ __launch_bounds__(kWave * WPB) void rx_wave_kernel(KParams kp) {
+#ifndef MTCP_GPU_TESTING
+    static_assert(ABL == 0, "the ABL (profiling) variants need a -DMTCP_GPU_TESTING build (tools/)");
+#endif
     __shared__ uint4 lds[WPB][kSlotChunks];                // the frame's chunks 0..6
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -340,6 +343,9 @@ struct GroupShape {
 // starts on a 4-byte boundary (AL 0: never; an A/B baseline).
 template <int MODE, bool RSS, int G, int ABL = 0, int AL = 1>
 __global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
+#ifndef MTCP_GPU_TESTING
+    static_assert(ABL == 0, "the ABL (profiling) variants need a -DMTCP_GPU_TESTING build (tools/)");
+#endif
     using Sh = GroupShape<G>;
     constexpr int P = Sh::P, U = Sh::U, R = Sh::R, S = Sh::S;
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];

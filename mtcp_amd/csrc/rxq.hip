@@ -19,6 +19,7 @@
 
 #include <chrono>
 #include <new>
+#include <thread>
 
 #include "../../include/mtcp_gpu.h"
 #include "../../include/mtcp_gpu_rxq.h"
@@ -142,6 +143,23 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
 void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q) {
     if (!q) return;
     RxqDevice dg(q->device);
+    if (q->evt && q->abandoned) {
+        // a flush rxq_wait_for gave up on may still copy into buf / res /
+        // d_out: wait for it a bounded time; if the device still has not
+        // finished it, leave every buffer and the event allocated (never
+        // touched again) rather than free memory under its DMA, or block in
+        // a free that synchronises with a hung device
+        const auto deadline = std::chrono::steady_clock::now() +
+                              std::chrono::microseconds(MTCP_GPU_RXQ_DESTROY_WAIT_US);
+        hipError_t e;
+        while ((e = hipEventQuery(q->evt)) == hipErrorNotReady &&
+               std::chrono::steady_clock::now() < deadline)
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (e == hipErrorNotReady) {
+            delete q;
+            return;
+        }
+    }
     if (q->evt) {
         if (q->inflight) (void)hipEventSynchronize(q->evt);
         (void)hipEventDestroy(q->evt);
@@ -270,8 +288,10 @@ int mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n) {
     return mtcp_gpu_rxq_wait(q, n);
 }
 
-uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
-                          const mtcp_gpu_result **res) {
+namespace {
+// rxq_get / rxq_get16: frame i's record (rec bytes) through `rec_out`
+uint8_t *rxq_serve(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len, const uint8_t **rec_out) {
+    if (rec_out) *rec_out = nullptr;
     if (!q || i >= q->done_n) return nullptr;
     if (q->ahead && i + q->ahead < q->done_n) {
         serve_prefetch(q->buf + ((uint64_t)q->desc[i + q->ahead].offset << 6), q->hint);
@@ -282,7 +302,7 @@ uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
     const uint8_t verdict = r[q->rec == 16 ? offsetof(mtcp_gpu_result16, verdict)
                                            : offsetof(mtcp_gpu_result, verdict)];
     if (len) *len = q->desc[i].len;
-    if (res) *res = reinterpret_cast<const mtcp_gpu_result *>(r);
+    if (rec_out) *rec_out = r;
     // core.c:774-775 counts NULL as rx_errors: the checksum failures, and the
     // frames whose headers claim bytes past the frame (the reference would
     // read past len there; the GPU computed no checksum to vouch for them)
@@ -290,6 +310,26 @@ uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
         verdict == MTCP_GPU_V_TRUNCATED)
         return nullptr;
     return q->buf + ((uint64_t)q->desc[i].offset << 6);
+}
+}  // namespace
+
+uint8_t *mtcp_gpu_rxq_get(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
+                          const mtcp_gpu_result **res) {
+    const uint8_t *r = nullptr;
+    uint8_t *p = rxq_serve(q, i, len, res ? &r : nullptr);
+    // a 16 B record is not a mtcp_gpu_result: never hand it out as one
+    if (res) *res = q && q->rec == sizeof(mtcp_gpu_result) ? reinterpret_cast<const mtcp_gpu_result *>(r) : nullptr;
+    return p;
+}
+
+uint8_t *mtcp_gpu_rxq_get16(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len,
+                            const mtcp_gpu_result16 **res16) {
+    const uint8_t *r = nullptr;
+    uint8_t *p = rxq_serve(q, i, len, res16 ? &r : nullptr);
+    if (res16)
+        *res16 = q && q->rec == sizeof(mtcp_gpu_result16) ? reinterpret_cast<const mtcp_gpu_result16 *>(r)
+                                                          : nullptr;
+    return p;
 }
 
 uint8_t *mtcp_gpu_rxq_frame(mtcp_gpu_rxq *q, uint32_t i, uint16_t *len) {

@@ -38,10 +38,11 @@
  * dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers 0 while the GPU path
  * of that interface is healthy and -1 otherwise, so mTCP falls back to its
  * own checksums exactly as with a NIC that lacks the offload
- * (dpdk_dev_ioctl, dpdk_module.c:809-816).  Every wait for an aggregate is
- * bounded (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000, 0: none): a GPU that
- * stops answering is abandoned, never waited on again, and mTCP checks every
- * frame from then on.
+ * (dpdk_dev_ioctl, dpdk_module.c:809-816).  On the receive side every wait
+ * on the GPU is bounded (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000, 0: none;
+ * clamped to 4294967): a GPU that stops answering is abandoned, never waited
+ * on again, and mTCP checks every frame from then on.  (The opt-in transmit
+ * fill below is synchronous and not bounded.)
  * NETSTAT: a frame dropped here never reaches ProcessPacket, so get_rptr
  * counts it in rx_packets / rx_bytes as ProcessPacket would have
  * (eth_in.c:20-23) and core.c:774-775 counts the NULL in rx_errors: the three
@@ -65,10 +66,18 @@
  * dealt round-robin among that node's devices (gpu_topo.h; mTCP binds each
  * thread's memory to its core's node, mtcp/src/cpu.c:54-79, and DPDK puts
  * each port's queues on the NIC's socket, dpdk_module.c:660-663);
- * MTCP_GPU_DEVICE=d forces one.  MTCP_GPU_THREADS=k: only the first k
- * threads to start on a device offload (the rest pass through and mTCP
- * checks their frames itself): past two threads a GPU's PCIe link is full
- * (DESIGN.md §5).
+ * MTCP_GPU_DEVICE=d forces one.  Admission: at most GPU_THREADS_DEFAULT
+ * (2) mTCP threads per GPU offload; the others pass through and mTCP checks
+ * their frames itself (dev_ioctl -1), as dpdk_module.c claims an offload
+ * only where the device has it (dpdk_module.c:809-816): past two threads a
+ * GPU's PCIe link is full and an offloading thread waits on it while its
+ * core could check the frames.  MTCP_GPU_THREADS=k sets
+ * another limit, MTCP_GPU_THREADS=all admits every thread.
+ *
+ * Fault injection (MTCP_GPU_FAIL_AFTER, MTCP_GPU_STALL_AFTER /
+ * MTCP_GPU_STALL_US) exists only in test builds (-DMTCP_GPU_TESTING, linked
+ * with tests/c/libmtcp_gpu_testing.so); a production build ignores those
+ * variables.
  *
  * Resources per mTCP thread: one GPU context (one HIP stream), and, for each
  * of the CONFIG.eths_num interfaces (mtcp.h:138), two rxqs (pinned staging
@@ -89,6 +98,9 @@
 #include "mtcp_gpu.h"
 #include "mtcp_gpu_rxq.h"
 #include "gpu_topo.h"
+#ifdef MTCP_GPU_TESTING
+#include "mtcp_gpu_testing.h"     /* mtcp_gpu_debug_stall (tests/c) */
+#endif
 
 #define GPU_AGG_BURSTS 64                 /* bursts per GPU launch           */
 #define GPU_BURST      64                 /* PS_CHUNK_SIZE / MAX_PKT_BURST   */
@@ -96,6 +108,7 @@
 #define GPU_FRAME_MAX  2048ull            /* MAX_PACKET_SIZE (ps.h:173)      */
 #define GPU_FRAME_JUMBO 9216ull           /* the largest frame a burst is expected to bring */
 #define GPU_TX_MAX     4096               /* frames recorded between two send_pkts */
+#define GPU_THREADS_DEFAULT 2             /* offloading threads per GPU */
 
 /* the backend being wrapped (e.g. &ps_module_func or &dpdk_module_func) */
 io_module_func *gpu_inner_module;
@@ -137,10 +150,13 @@ struct gpu_private_context {
     int passthrough;                      /* no GPU at init: the inner backend */
     int pipeline;                         /* serve aggregate k while k+1 is checked */
     int tx;                               /* tx checksums filled here        */
+#ifdef MTCP_GPU_TESTING
     long fail_after;                      /* MTCP_GPU_FAIL_AFTER: fault injection, -1 off */
     long stall_after;                     /* MTCP_GPU_STALL_AFTER: fault injection, -1 off */
     uint32_t stall_us;                    /* MTCP_GPU_STALL_US                */
+#endif
     uint32_t wait_us;                     /* MTCP_GPU_WAIT_TIMEOUT_MS, 0: no limit */
+    int slot_dev;                         /* device whose admission slot this thread holds, -1 */
     mtcp_gpu_ctx *hung;                   /* abandoned after a timed-out wait: never waited on */
     long launches;                        /* aggregates sent to the GPU       */
     struct gpu_ifq *ifq[MAX_DEVICES];     /* created at init (or first recv_pkts) */
@@ -150,14 +166,6 @@ struct gpu_private_context {
 
 /* a context for threads whose own allocation failed: passthrough only */
 static __thread struct gpu_private_context gpu_fallback_ctx;
-
-static void gpu_ifq_wait(struct gpu_ifq *f)
-{
-    int b;
-    for (b = 0; b < 2; b++)
-        if (f->rxq[b])
-            (void)mtcp_gpu_rxq_wait(f->rxq[b], NULL);
-}
 
 /* A wait ran past MTCP_GPU_WAIT_TIMEOUT_MS: the GPU is not answering.
  * Software checksums from now on, without waiting for it again: every
@@ -179,15 +187,22 @@ static void gpu_abandon(struct gpu_private_context *g)
                 }
 }
 
-/* After any GPU error: let the queued work finish, then software checksums
- * from now on (dev_ioctl answers -1). */
+/* After any GPU error: let the queued work finish (each wait bounded by
+ * MTCP_GPU_WAIT_TIMEOUT_MS: a device that does not finish it is abandoned
+ * instead), then software checksums from now on (dev_ioctl answers -1). */
 static void gpu_fail(struct gpu_private_context *g)
 {
-    int i;
+    int i, b;
     TRACE_ERROR("gpu_module: GPU path failed; software checksums from now on\n");
     for (i = 0; i < MAX_DEVICES; i++)
         if (g->ifq[i])
-            gpu_ifq_wait(g->ifq[i]);
+            for (b = 0; b < 2; b++)
+                if (g->ifq[i]->rxq[b] &&
+                    mtcp_gpu_rxq_wait_for(g->ifq[i]->rxq[b], NULL, g->wait_us) == MTCP_GPU_ETIMEDOUT &&
+                    g->gpu) {
+                    gpu_abandon(g);              /* never waited on (or closed) again */
+                    return;
+                }
     if (g->gpu)
         mtcp_gpu_close(g->gpu);
     g->gpu = NULL;
@@ -269,19 +284,54 @@ static int gpu_pick_device(int cpu, int ndev)
     return gpu_topo_pick(cpu, node, rank, ndev, dev_node);
 }
 
-/* MTCP_GPU_THREADS=k: at most k mTCP threads per GPU offload; the others
- * run on the wrapped backend alone (dev_ioctl -1: mTCP's own checksums).
- * One GPU's PCIe link carries the frames of about two threads (DESIGN.md
- * §5), so threads beyond that wait on the link while their cores could
- * check frames themselves.  Unset: every thread offloads. */
+/* Admission: at most k mTCP threads per GPU offload; the others run on the
+ * wrapped backend alone (dev_ioctl -1: mTCP's own checksums).  One GPU's
+ * PCIe link carries the frames of about two threads, so
+ * threads beyond that would wait on the link while their cores could check
+ * frames themselves.  k = GPU_THREADS_DEFAULT unless MTCP_GPU_THREADS says
+ * otherwise ("all": no limit).  A thread holds its slot from a successful
+ * open until destroy_handle (gpu_thread_release). */
 static int gpu_thread_count[GPU_TOPO_MAX_DEVS];
 
-static int gpu_thread_admitted(int dev)
+static int gpu_thread_limit(void)
 {
     const char *lim = getenv("MTCP_GPU_THREADS");
-    if (!lim || !*lim || dev >= GPU_TOPO_MAX_DEVS)
+    if (!lim || !*lim)
+        return GPU_THREADS_DEFAULT;
+    if (strcmp(lim, "all") == 0)
+        return -1;
+    return atoi(lim) < 0 ? 0 : atoi(lim);
+}
+
+static int gpu_thread_admit(int dev)
+{
+    const int lim = gpu_thread_limit();         /* -1: no limit (still counted) */
+    if (dev < 0 || dev >= GPU_TOPO_MAX_DEVS)
         return 1;
-    return __sync_fetch_and_add(&gpu_thread_count[dev], 1) < atoi(lim);
+    if (__sync_add_and_fetch(&gpu_thread_count[dev], 1) <= lim || lim < 0)
+        return 1;
+    __sync_sub_and_fetch(&gpu_thread_count[dev], 1);
+    return 0;
+}
+
+static void gpu_thread_release(struct gpu_private_context *g)
+{
+    if (g->slot_dev >= 0 && g->slot_dev < GPU_TOPO_MAX_DEVS)
+        __sync_sub_and_fetch(&gpu_thread_count[g->slot_dev], 1);
+    g->slot_dev = -1;
+}
+
+/* MTCP_GPU_WAIT_TIMEOUT_MS in microseconds: default 2000 ms; negative or 0:
+ * no limit; at most 4294967 ms (the limit is a 32-bit count of us) */
+static uint32_t gpu_wait_us(void)
+{
+    const char *e = getenv("MTCP_GPU_WAIT_TIMEOUT_MS");
+    long long ms = e && *e ? strtoll(e, NULL, 10) : 2000;
+    if (ms <= 0)
+        return 0;
+    if (ms > 4294967ll)
+        ms = 4294967ll;
+    return (uint32_t)(ms * 1000);
 }
 
 static void gpu_init_handle(struct mtcp_thread_context *ctx)
@@ -298,24 +348,26 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
         memset(g, 0, sizeof(*g));
         g->passthrough = 1;
     }
+    g->slot_dev = -1;
     g->inner = ctx->io_private_context;
     ctx->io_private_context = g;
     if (g->passthrough)
         return;
     g->pipeline = !(pl && strcmp(pl, "0") == 0);
     g->tx = tx && strcmp(tx, "1") == 0;
+#ifdef MTCP_GPU_TESTING
     /* MTCP_GPU_FAIL_AFTER=k: the (k+1)-th aggregate's launch fails as a GPU
      * error would, so the fallback to mTCP's own checksums is exercised on a
      * healthy GPU (tests/test_dropin.py) */
     g->fail_after = getenv("MTCP_GPU_FAIL_AFTER") ? atol(getenv("MTCP_GPU_FAIL_AFTER")) : -1;
     /* MTCP_GPU_STALL_AFTER=k, MTCP_GPU_STALL_US=u: the (k+1)-th aggregate
      * waits u us on the GPU behind mtcp_gpu_debug_stall, so that the wait
-     * limit (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000; 0: none) and the
-     * fallback after it are exercised on a healthy GPU */
+     * limit (MTCP_GPU_WAIT_TIMEOUT_MS) and the fallback after it are
+     * exercised on a healthy GPU */
     g->stall_after = getenv("MTCP_GPU_STALL_AFTER") ? atol(getenv("MTCP_GPU_STALL_AFTER")) : -1;
     g->stall_us = getenv("MTCP_GPU_STALL_US") ? (uint32_t)atol(getenv("MTCP_GPU_STALL_US")) : 0;
-    g->wait_us = 1000u * (uint32_t)(getenv("MTCP_GPU_WAIT_TIMEOUT_MS") ? atol(getenv("MTCP_GPU_WAIT_TIMEOUT_MS"))
-                                                                     : 2000);
+#endif
+    g->wait_us = gpu_wait_us();
     if (g->tx && !gpu_tx_capable(gpu_inner_module)) {
         TRACE_ERROR("gpu_module: MTCP_GPU_TX=1 refused: the wrapped backend sends from get_wptr\n");
         g->tx = 0;
@@ -323,10 +375,11 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 
     ndev = mtcp_gpu_device_count();
     dev = ndev > 0 ? gpu_pick_device(ctx->cpu, ndev) : -1;
-    if (dev >= 0 && !gpu_thread_admitted(dev)) {
+    if (dev >= 0 && !gpu_thread_admit(dev)) {
         g->passthrough = 1;                  /* mTCP's own checksums on this core */
         return;
     }
+    g->slot_dev = dev;
     /* compact 16 B records: the rxqs read the verdict only (40 -> 16 B of D2H per frame) */
     if (dev < 0 || mtcp_gpu_open(&g->gpu, dev, NULL, 1, MTCP_GPU_F_COMPACT) != MTCP_GPU_OK ||
         mtcp_gpu_reserve(g->gpu, 0, 0) != MTCP_GPU_OK) {     /* load the kernels now */
@@ -334,6 +387,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
             mtcp_gpu_close(g->gpu);
         g->gpu = NULL;
         g->passthrough = 1;                  /* behave exactly like the inner */
+        gpu_thread_release(g);               /* the slot goes to a thread that opens */
         return;
     }
     for (i = 0; i < CONFIG.eths_num && i < MAX_DEVICES; i++)
@@ -478,10 +532,13 @@ static uint32_t gather(struct mtcp_thread_context *ctx, struct gpu_ifq *f, int i
     f->count[a] = total;
     f->launched[a] = 0;
     if (total && g->gpu) {
+        int inject_fail = 0;
+#ifdef MTCP_GPU_TESTING
         if (g->launches == g->stall_after)
             (void)mtcp_gpu_debug_stall(g->gpu, g->stall_us);
-        if ((g->fail_after < 0 || g->launches < g->fail_after) &&
-            mtcp_gpu_rxq_flush_async(q) == MTCP_GPU_OK) {
+        inject_fail = g->fail_after >= 0 && g->launches >= g->fail_after;
+#endif
+        if (!inject_fail && mtcp_gpu_rxq_flush_async(q) == MTCP_GPU_OK) {
             f->launched[a] = 1;
             g->launches++;
         } else {
@@ -593,6 +650,7 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
     }
     if (g->gpu)
         mtcp_gpu_close(g->gpu);
+    gpu_thread_release(g);
     INNER_VOID(ctx, gpu_inner_module->destroy_handle(ctx));
     ctx->io_private_context = g->inner;
     if (g != &gpu_fallback_ctx)

@@ -44,3 +44,45 @@ def make_shard(n: int, size, rank: int, world: int, seed: int = 0, off_shift: in
     lens = pktgen.lengths(count, size, seed, first_index=first)
     desc, nbytes = pktgen.layout_from_lengths(lens, off_shift)
     return Shard(rank, world, first, count, desc, nbytes)
+
+
+def core_groups(cpus, sysfs: str = "/sys") -> list[list[int]]:
+    """`cpus` grouped into physical cores (sysfs
+    devices/system/cpu/cpuN/topology/thread_siblings_list), ordered by each
+    core's lowest cpu id; a cpu whose topology sysfs does not give is a core
+    of its own."""
+    import os
+    from .gpu import parse_cpulist
+    cpus = set(cpus)
+    seen: set[int] = set()
+    groups: list[list[int]] = []
+    for c in sorted(cpus):
+        if c in seen:
+            continue
+        try:
+            with open(os.path.join(sysfs, "devices", "system", "cpu", f"cpu{c}", "topology",
+                                   "thread_siblings_list")) as f:
+                sib = parse_cpulist(f.read()) & cpus
+        except (OSError, ValueError):
+            sib = set()
+        g = sorted(sib | {c})
+        seen.update(g)
+        groups.append(g)
+    return groups
+
+
+def split_cpus(cpus, index: int, k: int, sysfs: str = "/sys") -> set[int]:
+    """The `index`-th of `k` disjoint shares of `cpus`, in whole physical
+    cores (no two shares hold SMT siblings of one core): the share-nothing
+    split mTCP makes of a node's cores among its per-queue threads
+    (mtcp/src/core.c:1195-1213, one thread per core; dpdk_module.c:644-676,
+    one queue per thread).  bench.py gives every rank whose GPU sits on the
+    same node one share, so that the ranks' concurrent CPU baselines do not
+    time the same cores.  With fewer cores than shares the shares wrap."""
+    groups = core_groups(cpus, sysfs)
+    if not groups or k <= 1:
+        return set(cpus)
+    if len(groups) < k:
+        return set(groups[index % len(groups)])
+    lo, hi = len(groups) * index // k, len(groups) * (index + 1) // k
+    return {c for g in groups[lo:hi] for c in g}

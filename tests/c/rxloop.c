@@ -30,11 +30,19 @@
  *            may run on, as mtcp_core_affinitize (cpu.c) pins each mTCP
  *            thread to its core (RXLOOP_CPUS=a,b,..: thread t on the t-th
  *            CPU of that list; RXLOOP_PIN=0: unpinned)
+ *   RXLOOP_PASSES=p  (timing modes) each thread's backend serves its shard p
+ *            times over, so that a run lasts long enough to time many threads
+ *   RXLOOP_REF=lib   (timing modes) the software checks of a thread the module
+ *            does not offload (dev_ioctl -1) are the REFERENCE's own
+ *            ProcessPacket chain (oracle/_ref/libref_rx.so, ref_rx_packet:
+ *            eth_in / ip_in / tcp_in / tcp_util compiled from /root/reference),
+ *            not the oracle's restatement
  * Prints one JSON line with the counters and the wall time of the rx loop
  * (tools/io_path_bench.py turns that into the io_module path's rate).  Built with the test doubles in
  * tests/c/mtcp_double (two fields of mtcp_thread_context, io_module_func).
  */
 #define _GNU_SOURCE
+#include <dlfcn.h>
 #include <pthread.h>
 #include <sched.h>
 #include <stdio.h>
@@ -60,10 +68,16 @@ extern io_module_func gpu_module_func;
 struct mtcp_config CONFIG = {1};                   /* one interface (mtcp.conf's port list) */
 extern io_module_func *gpu_inner_module;
 
+/* RXLOOP_REF: the reference's rx chain (ref_glue.h's ref_rx_packet) */
+typedef int (*ref_rx_fn)(unsigned char *pkt, int len, int *ret_out, uint16_t *tcp_csum);
+static ref_rx_fn g_ref_rx;
+enum { REF_BR_IP_CSUM_BAD = 4, REF_BR_TCP_CSUM_BAD = 9 };   /* oracle/ref/ref_glue.h */
+
 struct fake_psio {
     const uint8_t *buf;
     const mtcp_gpu_desc *desc;
     uint32_t n, next, base, cnt;
+    uint32_t passes_left;            /* RXLOOP_PASSES - 1: serve the shard again */
     int recv_calls;
     uint8_t *tx_buf;                 /* tx: frame i is written at desc[i].offset */
     uint32_t tx_next, tx_queued, tx_sent;
@@ -104,6 +118,10 @@ static int32_t fake_recv(struct mtcp_thread_context *ctx, int ifidx)
     (void)ifidx;
     if (f != tl_fake) { fprintf(stderr, "context swap broken\n"); exit(3); }
     f->recv_calls++;
+    if (f->next == f->n && f->passes_left) {
+        f->passes_left--;
+        f->next = 0;
+    }
     f->base = f->next;
     f->cnt = f->n - f->next < 64 ? f->n - f->next : 64;
     f->next += f->cnt;
@@ -228,7 +246,7 @@ static void *worker_main(void *arg)
              * and the module has returned nothing twice (a pipelined module
              * returns 0 while it fills, and its last aggregate one call
              * after the backend ran dry) */
-            if (f->next == f->n && ++idle >= 2)
+            if (f->next == f->n && !f->passes_left && ++idle >= 2)
                 break;
             continue;
         }
@@ -242,8 +260,17 @@ static void *worker_main(void *arg)
         for (i = 0; i < recv_cnt; i++) {
             uint16_t len = 0;
             uint8_t *pktbuf = gpu_module_func.get_rptr(&ctx, 0, i, &len);
-            const mtcp_gpu_desc *d = &f->desc[w->seen + (uint32_t)i];
-            if (pktbuf != NULL && sw) {
+            const uint32_t at = (w->seen + (uint32_t)i) % f->n;   /* RXLOOP_PASSES wraps */
+            const mtcp_gpu_desc *d = &f->desc[at];
+            if (pktbuf != NULL && sw && g_ref_rx) {
+                int ret;
+                uint16_t csum;
+                const int br = g_ref_rx(pktbuf, len, &ret, &csum);
+                if (br == REF_BR_IP_CSUM_BAD || br == REF_BR_TCP_CSUM_BAD)
+                    pktbuf = NULL;                     /* ERROR: counted in rx_errors */
+                else
+                    w->hdr_sum += csum;
+            } else if (pktbuf != NULL && sw) {
                 mtcp_gpu_result r;
                 const int v = oracle_rx_packet(pktbuf, len, NULL, &r);
                 if (v == MTCP_GPU_V_IP_CSUM_BAD || v == MTCP_GPU_V_TCP_CSUM_BAD || v == MTCP_GPU_V_TRUNCATED)
@@ -258,7 +285,7 @@ static void *worker_main(void *arg)
                      * would (first 64 B), no byte-for-byte check */
                     uint32_t k;
                     for (k = 0; k < 64 && k < len; k += 8) w->hdr_sum += pktbuf[k];
-                    w->status[w->seen + i] = 1;
+                    w->status[at] = 1;
                 } else if (w->timing == 2) {
                     /* payload mode: read every byte once, as the payload's copy
                      * into the stream's receive buffer would (tcp_in.c ->
@@ -271,10 +298,10 @@ static void *worker_main(void *arg)
                         acc += v;
                     }
                     w->hdr_sum += acc;
-                    w->status[w->seen + i] = 1;
+                    w->status[at] = 1;
                 } else {
                     int same = len == d->len && memcmp(pktbuf, f->buf + d->offset, len) == 0;
-                    w->status[w->seen + i] = same ? 1 : 2;
+                    w->status[at] = same ? 1 : 2;
                     w->changed += !same;
                 }
                 w->rx_packets++;
@@ -341,6 +368,14 @@ int main(int argc, char **argv)
         for (t = 0; t < threads && cnt; t++) pin_cpu[t] = list[t % cnt];
     }
 
+    const char *passes_env = getenv("RXLOOP_PASSES");
+    const uint32_t passes = passes_env && atoi(passes_env) > 1 && timing ? (uint32_t)atoi(passes_env) : 1;
+    const char *ref_env = getenv("RXLOOP_REF");
+    if (ref_env && *ref_env) {
+        void *h = dlopen(ref_env, RTLD_NOW | RTLD_LOCAL);
+        g_ref_rx = h ? (ref_rx_fn)dlsym(h, "ref_rx_packet") : NULL;
+        if (!g_ref_rx) { fprintf(stderr, "RXLOOP_REF: %s\n", dlerror()); return 1; }
+    }
     gpu_inner_module = &fake_module;
     if (getenv("RXLOOP_AS_NETMAP") && strcmp(getenv("RXLOOP_AS_NETMAP"), "1") == 0) {
         netmap_module_func = fake_module;
@@ -362,6 +397,7 @@ int main(int argc, char **argv)
         w->fake.buf = buf;
         w->fake.desc = desc + lo;
         w->fake.n = hi - lo;
+        w->fake.passes_left = passes - 1;
         if (pthread_create(&w->tid, NULL, worker_main, w) != 0) { perror("pthread_create"); return 1; }
     }
     t1 = g_t0;
@@ -411,11 +447,11 @@ int main(int argc, char **argv)
            "\"rx_packets\": %llu, \"rx_errors\": %llu, \"changed\": %llu, "
            "\"ioctl_rx_ip\": %d, \"ioctl_rx_tcp\": %d, \"seconds\": %.6f, "
            "\"frame_bytes\": %llu, \"timing_mode\": %d, \"hdr_sum\": %llu, \"threads\": %d, "
-           "\"offloading_threads\": %d}\n",
+           "\"offloading_threads\": %d, \"passes\": %u, \"sw_checks\": \"%s\"}\n",
            n, seen, rounds, recv_calls, (unsigned long long)rx_packets,
            (unsigned long long)rx_errors, (unsigned long long)changed, ws[0].ioctl_ip,
            ws[0].ioctl_tcp, secs, (unsigned long long)frame_bytes, timing,
-           (unsigned long long)hdr_sum, threads, offloading);
+           (unsigned long long)hdr_sum, threads, offloading, passes, g_ref_rx ? "reference" : "oracle");
     free(ws);
     free(status);
     free((void *)buf);

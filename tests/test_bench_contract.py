@@ -35,6 +35,39 @@ def test_default_run_is_c2_on_one_gpu(bench, monkeypatch):
     assert a.steps > 0 and a.warmup >= 0
 
 
+@pytest.mark.parametrize("gpus", [2, 4, 8])
+def test_default_run_on_n_gpus_is_c4(bench, monkeypatch, gpus):
+    """`bench.py --gpus N` (the driver's form) runs BASELINE.json's
+    multi-GPU config: C4's 2 M x 1500 B per GPU, 16 M in total at N = 8."""
+    monkeypatch.setattr("sys.argv", ["bench.py", "--gpus", str(gpus)])
+    a = bench.parse()
+    assert a.config == "c4" and not a.strong
+    w = bench.workload(a.config, gpus)
+    assert (w["per_gpu"], w["total"], w["scaling"]) == (1 << 21, gpus << 21, "weak")
+    assert w["desc"].startswith(f"c4: {2 * gpus} M x 1500 B")
+    assert f"2 M per GPU x {gpus} MI355X" in w["desc"]
+
+
+def test_workload_arithmetic(bench):
+    w = bench.workload("c2", 1)
+    assert (w["per_gpu"], w["total"], w["scaling"]) == (1 << 20, 1 << 20, "weak")
+    assert w["desc"].startswith("c2: 1 M x 1500 B") and w["desc"].endswith("1 MI355X")
+    w = bench.workload("c4", 8)
+    assert (w["per_gpu"], w["total"]) == (1 << 21, 1 << 24)
+    assert w["desc"].startswith("c4: 16 M x 1500 B")
+    # --strong: C4's 16 M batch split N ways
+    for n in (1, 2, 4, 8):
+        w = bench.workload("c4", n, strong=True)
+        assert (w["total"], w["per_gpu"] * n, w["scaling"]) == (1 << 24, 1 << 24, "strong")
+    w = bench.workload("c5", 8, strong=True)
+    assert (w["total"], w["per_gpu"]) == (4 << 20, 512 << 10)
+    w = bench.workload("c3", 2, strong=True)
+    assert (w["total"], w["per_gpu"]) == (1 << 20, 1 << 19) and "bimodal" in w["desc"]
+    # --per-gpu (tests) overrides, weak
+    w = bench.workload("c4", 2, per_gpu_override=1 << 17)
+    assert (w["total"], w["scaling"]) == (1 << 18, "weak") and w["desc"].startswith("c4: 256 K")
+
+
 def test_rows_refuse_multi_gpu(bench, monkeypatch):
     monkeypatch.setattr("sys.argv", ["bench.py", "--config", "f1", "--gpus", "2"])
     with pytest.raises(SystemExit):

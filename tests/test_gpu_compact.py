@@ -189,14 +189,29 @@ def test_compact_rxq_drops_the_same_frames(gpu, golden):
             nulls = np.zeros(len(golden.desc), bool)
             verdicts = np.zeros(len(golden.desc), np.uint8)
             for i in range(len(golden.desc)):
-                ln, res = ctypes.c_uint16(), ctypes.c_void_p()
-                p = L.mtcp_gpu_rxq_get(q, i, ctypes.byref(ln), ctypes.byref(res))
+                ln, res, res40 = ctypes.c_uint16(), ctypes.c_void_p(), ctypes.c_void_p(1)
+                p = L.mtcp_gpu_rxq_get16(q, i, ctypes.byref(ln), ctypes.byref(res))
                 nulls[i] = p is None
                 verdicts[i] = ctypes.cast(res, ctypes.POINTER(ctypes.c_uint8))[14]
+                # the 40 B accessor never hands out a 16 B record
+                assert L.mtcp_gpu_rxq_get(q, i, None, ctypes.byref(res40)) == p
+                assert res40.value is None
         finally:
             L.mtcp_gpu_rxq_destroy(q)
     drop = (ok & np.isin(ref_v, [4, 9])) | (golden.meta["ref_ub"] == 1)
     assert np.array_equal(nulls, drop)
+    # and rxq_get16 on a 40 B context: no record
+    with gpu.Context(0) as ctx:
+        q = ctypes.c_void_p()
+        assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 64, 64 * 2048) == 0
+        try:
+            assert L.mtcp_gpu_rxq_push_chunk(q, golden.buf.ctypes.data, golden.desc.ctypes.data, 64, 0) == 0
+            assert L.mtcp_gpu_rxq_flush(q, None) == 0
+            res16 = ctypes.c_void_p(1)
+            L.mtcp_gpu_rxq_get16(q, 0, None, ctypes.byref(res16))
+            assert res16.value is None
+        finally:
+            L.mtcp_gpu_rxq_destroy(q)
     assert np.array_equal(verdicts[ok], ref_v[ok])
 
 

@@ -6,6 +6,7 @@ the frames whose headers claim bytes past the frame (TRUNCATED), the staged
 frame byte for byte otherwise, and every result record equal to the
 oracle's for the same frame."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -17,6 +18,16 @@ torch = pytest.importorskip("torch")
 
 V_IP_CSUM_BAD, V_TCP_CSUM_BAD, V_TRUNCATED, V_BAD_DESC = 4, 9, 10, 11
 EINVAL = -22
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def testing_lib():
+    """tests/c/libmtcp_gpu_testing.so: mtcp_gpu_debug_stall, the fault
+    injection the product library does not export (built by build())."""
+    T = ctypes.CDLL(os.path.join(ROOT, "tests", "c", "libmtcp_gpu_testing.so"))
+    T.mtcp_gpu_debug_stall.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    T.mtcp_gpu_debug_stall.restype = ctypes.c_int
+    return T
 
 
 @pytest.mark.gpu
@@ -83,13 +94,13 @@ def test_rxq_wait_for_abandons_a_flush_that_does_not_finish(golden):
     import time
     from mtcp_amd import gpu
     from mtcp_amd._lib import lib
-    L = lib()
+    L, T = lib(), testing_lib()
     ETIMEDOUT, EIO = -110, -5
     buf, desc = golden.buf, golden.desc
     base = buf.ctypes.data
     part = desc[:256]
     with gpu.Context(0) as ctx:
-        assert L.mtcp_gpu_debug_stall(ctx._h, 20 * 1000 * 1000) == EINVAL     # over the 10 s cap
+        assert T.mtcp_gpu_debug_stall(ctx._h, 20 * 1000 * 1000) == EINVAL     # over the 10 s cap
         q = ctypes.c_void_p()
         assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 256, 256 * 2048) == 0
         try:
@@ -102,7 +113,7 @@ def test_rxq_wait_for_abandons_a_flush_that_does_not_finish(golden):
             L.mtcp_gpu_rxq_reset(q)
             for d in part:
                 assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
-            assert L.mtcp_gpu_debug_stall(ctx._h, 300 * 1000) == 0
+            assert T.mtcp_gpu_debug_stall(ctx._h, 300 * 1000) == 0
             t0 = time.monotonic()
             assert L.mtcp_gpu_rxq_flush_async(q) == 0
             assert L.mtcp_gpu_rxq_wait_for(q, ctypes.byref(n_done), 20 * 1000) == ETIMEDOUT
@@ -119,5 +130,51 @@ def test_rxq_wait_for_abandons_a_flush_that_does_not_finish(golden):
             assert L.mtcp_gpu_rxq_flush_async(q) == EIO
             assert L.mtcp_gpu_sync(ctx._h) == 0                  # the stall ends by itself
             assert time.monotonic() - t0 >= 0.25
+        finally:
+            L.mtcp_gpu_rxq_destroy(q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stall_ms,leaks", [(400, True), (60, False)])
+def test_rxq_destroy_right_after_a_timeout(golden, stall_ms, leaks):
+    """mtcp_gpu_rxq_destroy straight after MTCP_GPU_ETIMEDOUT, no
+    mtcp_gpu_sync first.  The abandoned flush may still write the staging:
+    destroy waits for it at most MTCP_GPU_RXQ_DESTROY_WAIT_US (100 ms).  A
+    400 ms stall outlasts that, so destroy returns in about 100 ms without
+    freeing (the buffers are leaked, the flush lands in them later); a 60 ms
+    stall ends within it, so destroy frees normally.  Either way the context
+    stays usable."""
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    import time
+    from mtcp_amd import gpu
+    from mtcp_amd._lib import lib
+    L, T = lib(), testing_lib()
+    buf, desc = golden.buf, golden.desc
+    base = buf.ctypes.data
+    with gpu.Context(0) as ctx:
+        q = ctypes.c_void_p()
+        assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 256, 256 * 2048) == 0
+        for d in desc[:256]:
+            assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
+        assert T.mtcp_gpu_debug_stall(ctx._h, stall_ms * 1000) == 0
+        assert L.mtcp_gpu_rxq_flush_async(q) == 0
+        assert L.mtcp_gpu_rxq_wait_for(q, None, 10 * 1000) == -110
+        t0 = time.monotonic()
+        L.mtcp_gpu_rxq_destroy(q)
+        dt = time.monotonic() - t0
+        if leaks:
+            assert 0.09 <= dt < 0.3, dt
+        else:
+            assert dt < 0.1, dt
+        assert L.mtcp_gpu_sync(ctx._h) == 0
+        # the context still works: a fresh rxq checks frames
+        q = ctypes.c_void_p()
+        assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 64, 64 * 2048) == 0
+        try:
+            for d in desc[:64]:
+                assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
+            n = ctypes.c_uint32()
+            assert L.mtcp_gpu_rxq_flush(q, ctypes.byref(n)) == 0 and n.value == 64
         finally:
             L.mtcp_gpu_rxq_destroy(q)

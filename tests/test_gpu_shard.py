@@ -125,3 +125,26 @@ def test_bench_two_ranks_equal_one_launch(gpu, tmp_path, config, size, rss, per_
     if size == "bimodal":                  # the byte-balanced split of shard.bounds
         cut = metas[1]["first_index"]
         assert cut == shard.bounds(n, size, 2, seed)[1]
+
+
+def test_bench_default_n2_runs_c4_with_cpu_baseline(gpu, tmp_path):
+    """The driver's N > 1 form without --config, launcher-less: the ranks run
+    BASELINE's multi-GPU config C4 (here at a reduced per-GPU count) and the
+    line carries the same-run CPU baseline of every rank on its own cores."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MTCP_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--per-gpu", str(1 << 17),
+           "--steps", "3", "--warmup", "1", "--cpu-sample", str(1 << 14), "--pcie", "off"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["workload"].startswith("c4: 256 K x 1500 B")
+    assert line["config"]["packets_total"] == 2 << 17
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["kind"] in ("reference", "port")
+    assert [r["rank"] for r in cb["per_rank"]] == [0, 1]
+    assert cb["cores"] == sum(r["cores"] for r in cb["per_rank"])
+    # the two ranks share device 0's node: disjoint halves of its cores
+    assert line["host_cpus"]["shared_with_ranks"] == [0, 1]

@@ -69,3 +69,39 @@ def test_two_rank_shards_equal_full_batch(size, world):
     buf, desc = _full(n, size, seed)
     want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(None, 4, 1))
     assert got == want.tobytes()
+
+
+def _fake_topology(root, ncores, smt):
+    """A sysfs tree with `ncores` physical cores of `smt` threads each,
+    numbered the Linux way (siblings ncores apart)."""
+    for c in range(ncores):
+        sib = ",".join(str(c + t * ncores) for t in range(smt))
+        for t in range(smt):
+            d = root / "devices" / "system" / "cpu" / f"cpu{c + t * ncores}" / "topology"
+            d.mkdir(parents=True)
+            (d / "thread_siblings_list").write_text(sib + "\n")
+
+
+def test_split_cpus_gives_disjoint_whole_cores(tmp_path):
+    """bench.py's N > 1 CPU baseline: ranks on one node split its cores in
+    whole physical cores (no two ranks time SMT siblings of one core)."""
+    _fake_topology(tmp_path, 64, 2)
+    node = set(range(128))
+    shares = [shard.split_cpus(node, i, 4, str(tmp_path)) for i in range(4)]
+    assert set().union(*shares) == node
+    for i, s in enumerate(shares):
+        assert len(s) == 32
+        prim = sorted(c for c in s if c < 64)
+        assert prim == list(range(16 * i, 16 * i + 16))
+        assert {c - 64 for c in s if c >= 64} == set(prim)      # siblings travel together
+        for t in shares[i + 1:]:
+            assert not s & t
+
+
+def test_split_cpus_edge_cases(tmp_path):
+    _fake_topology(tmp_path, 4, 1)
+    assert shard.split_cpus({0, 1, 2, 3}, 0, 1, str(tmp_path)) == {0, 1, 2, 3}
+    # more ranks than cores: the shares wrap
+    assert [shard.split_cpus({0, 1}, i, 4, str(tmp_path)) for i in range(4)] == [{0}, {1}, {0}, {1}]
+    # no topology in sysfs: every cpu is its own core
+    assert shard.split_cpus({5, 6, 7, 8}, 1, 2, str(tmp_path / "none")) == {7, 8}

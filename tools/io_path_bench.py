@@ -46,7 +46,7 @@ def frames(n, size, seed):
     return _frames[(n, size, seed)]
 
 
-def reference(n, size, seed):
+def reference(n, size, seed, cores_list=(1, 16)):
     """The reference's own rx code (eth_in/ip_in/tcp_in/tcp_util compiled from
     /root/reference into oracle/_ref) on the same frames: 1 and 16 cores."""
     import oracle   # the CPU baseline leg only
@@ -55,7 +55,7 @@ def reference(n, size, seed):
     desc, host = frames(n, size, seed)
     out = {"probe": "reference_rx", "frame_size": size, "frames": n}
     nbytes = int(desc["len"].astype(np.int64).sum())
-    for cores in (1, 16):
+    for cores in cores_list:
         t = oracle.ref_bench_rx(host.copy(), desc, 6, False, cores, 5)
         out[f"cores{cores}"] = {"mpkt_per_s": round(n / t / 1e6, 3), "GBs": round(nbytes / t / 1e9, 3)}
     return out
@@ -95,7 +95,7 @@ def host_topology():
             "gpu_pci": bdf, "gpu_numa_node": node, "gpu_local_cpus": local[:32]}
 
 
-def run(n, size, seed, tmp, mode, threads=1, pipeline=True, tx=True):
+def run(n, size, seed, tmp, mode, threads=1, pipeline=True, tx=True, reps=3):
     desc, host = frames(n, size, seed)
     bdesc = desc.copy()
     bdesc["offset"] = desc["offset"] << 6          # rxloop takes byte offsets
@@ -104,7 +104,7 @@ def run(n, size, seed, tmp, mode, threads=1, pipeline=True, tx=True):
     bdesc.tofile(dpath)
     exe = os.path.join(ROOT, "tests", "c", "rxloop")
     best = None
-    for _ in range(3):
+    for _ in range(reps):
         env = dict(os.environ, MTCP_GPU_PIPELINE="1" if pipeline else "0", MTCP_GPU_TX="1" if tx else "0")
         r = subprocess.run([exe, chunk, dpath, opath, mode, str(threads)],
                            capture_output=True, text=True, check=True, env=env)
@@ -122,9 +122,11 @@ def run(n, size, seed, tmp, mode, threads=1, pipeline=True, tx=True):
                         "(gather, H2D, kernel, D2H of 8 B per frame, check fields written back), "
                         "else mTCP's software fill per frame (here the oracle's restatement, "
                         "gcc -O2); wall clock, best of 3"}
+    n = n * best.get("passes", 1)            # RXLOOP_PASSES: the shard served p times
     return {"probe": "io_module_path", "mode": mode, "threads": threads, "pipeline": pipeline,
             "frame_size": size,
-            "frames": n,
+            "frames": n, "sw_checks": best.get("sw_checks"),
+            "offloading_threads": best.get("offloading_threads"),
             "bursts_per_launch": 64, "burst": 64, "seconds": s,
             "mpkt_per_s": round(n / s / 1e6, 3), "GBs": round(best["frame_bytes"] / s / 1e9, 3),
             "rx_errors": best["rx_errors"], "changed": best["changed"],
@@ -159,35 +161,47 @@ def main():
         dump(n, size, seeds.get(size, 7), sys.argv[3])
         return
     if "--hybrid" in sys.argv:
-        # MTCP_GPU_THREADS=k (gpu_module.c): k threads offload, the others
-        # check in software (rxloop's timing mode pays mTCP's own checks
-        # where dev_ioctl answers -1); every thread and the reference's own
-        # rx code pinned to the CPUs of the GPU's NUMA node; interleaved
+        # Admission (gpu_module.c): "default" = MTCP_GPU_THREADS unset (two
+        # threads per GPU offload), "0" = no thread offloads (mTCP on its
+        # own), k, "all".  A thread that does not offload runs the
+        # REFERENCE's own ProcessPacket chain on each frame (RXLOOP_REF =
+        # oracle/_ref/libref_rx.so) — so "0" is the reference's software
+        # path through the same loop.  Every thread pinned to the CPUs of the
+        # GPU's NUMA node; each thread's shard served RXLOOP_PASSES times (a
+        # run of ~0.3-1 s); interleaved; best of 2 per point.  The
+        # reference's own rx code alone (ref_bench_rx) at the same thread
+        # counts closes each size.
+        import oracle
         host = host_topology()
         print(json.dumps(host), flush=True)
         local = host["gpu_local_cpus"]
         saved = os.sched_getaffinity(0)
+        if oracle.ref_available():
+            os.environ["RXLOOP_REF"] = oracle.REF_LIB_PATH
         with tempfile.TemporaryDirectory() as tmp:
             for size in (1500, 64):
                 seed = 2 if size == 1500 else 1
                 for rep in range(2):
                     for threads in (4, 8, 16):
-                        for limit in ("all", "0", "1", "2", "4"):
+                        for limit in ("default", "0", "1", "2", "all"):
                             os.environ["RXLOOP_CPUS"] = ",".join(map(str, local))
+                            os.environ["RXLOOP_PASSES"] = str(4 * threads if size == 1500 else 2 * threads)
                             os.environ.pop("MTCP_GPU_THREADS", None)
-                            if limit != "all":
+                            if limit != "default":
                                 os.environ["MTCP_GPU_THREADS"] = limit
-                            r = run(n, size, seed, tmp, "timing", threads, True)
+                            r = run(n, size, seed, tmp, "timing", threads, True, reps=2)
                             print(json.dumps({"probe": "io_hybrid", "rep": rep, "frame_size": size,
                                               "threads": threads, "gpu_threads": limit,
-                                              "frames": n, "mpkt_per_s": r["mpkt_per_s"],
+                                              "offloading_threads": r["offloading_threads"],
+                                              "sw_checks": r["sw_checks"],
+                                              "frames": r["frames"], "mpkt_per_s": r["mpkt_per_s"],
                                               "GBs": r["GBs"], "rx_errors": r["rx_errors"]}),
                                   flush=True)
-                os.environ.pop("MTCP_GPU_THREADS", None)
-                os.environ.pop("RXLOOP_CPUS", None)
+                for k in ("MTCP_GPU_THREADS", "RXLOOP_CPUS", "RXLOOP_PASSES"):
+                    os.environ.pop(k, None)
                 os.sched_setaffinity(0, local)
                 try:
-                    ref = reference(n, size, seed)
+                    ref = reference(n, size, seed, (1, 4, 8, 16))
                 finally:
                     os.sched_setaffinity(0, saved)
                 if ref:
