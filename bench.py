@@ -581,14 +581,41 @@ def run_row(args):
         base_h, daddr_h, dport_h = 0x0A000001, 0xC0A80001, 80
         step = lambda: ctx.rss_queue_map_dev(base_h, num_addr, daddr_h, dport_h, nq, True, queue,
                                              stream=stream)
-        wall, kern = _timed(step, args.steps, args.warmup, stream)
+        # a launch is a few us: the K steps are captured in one HIP graph and
+        # replayed (a direct Python call per launch would time the host)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for _ in range(args.steps):
+                step()
+        graph.replay()
+        torch.cuda.synchronize()
+        wall, kern = _timed(graph.replay, 1, 0, stream)
+        wall, kern = wall / args.steps, kern / args.steps
         line.update(value=round(total / wall / 1e9, 3), unit="Gcandidates/s", dtype="u32",
                     ms_per_step=round(wall * 1e3, 5))
-        line["roofline"] = {"bound": "lds", "achieved": None, "peak": None, "unit": None,
-                            "frac": None, "traffic": None, "avg_launch_ms": round(kern * 1e3, 5),
-                            "note": "24 LDS nibble-table reads per candidate (Toeplitz over 96 "
-                                    "bits) and 1 B written: bound by LDS lookups, not HBM "
-                                    f"({total} B written per launch)"}
+        line["config"]["launch"] = "hip_graph"
+        # per candidate: 1 B written (the queue byte) — the HBM-side bytes;
+        # 3 LDS byte reads (C(i) ^ t_hi[port >> 8] ^ t_lo[port & 255], then the
+        # queue of the 7-bit value, flow_kernels.hpp): at ds_read_b32's
+        # 128 B/clk/CU x 256 CUs x 2.4 GHz = 78.6 TB/s (MI355X_MICROARCH.md
+        # §LDS; a byte read costs a dword read's cycle) that is 3 x 4 B per
+        # candidate
+        lds_peak = 128 * 256 * 2.4e9 / 1e9
+        lds_bytes = 12 * total
+        line["roofline"] = {"bound": "hbm", "achieved": round(total / kern / 1e9, 2), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(total / kern / 1e9 / HBM_PEAK_GBS, 4),
+                            "traffic": None, "kernel": "mg::rss_queue_map_kernel",
+                            "avg_launch_ms": round(kern * 1e3, 5), "algorithmic_bytes_per_launch": total,
+                            "lds": {"bytes_per_launch": lds_bytes, "achieved_GBs": round(lds_bytes / kern / 1e9, 1),
+                                    "peak_GBs": round(lds_peak, 1),
+                                    "frac": round(lds_bytes / kern / 1e9 / lds_peak, 4),
+                                    "note": "3 ds_read_u8 per candidate, priced as ds_read_b32 (128 B/clk/CU)"},
+                            "note": "1 B written per candidate is the only HBM traffic (the nibble tables "
+                                    "come from L2); at this size (4.1 MB) a launch is near the empty-kernel "
+                                    "floor (DESIGN §9: 2.0-2.7 us), so neither bound is reached"}
         import socket
         import struct
         b_n = struct.unpack("<I", socket.inet_aton("10.0.0.1"))[0]

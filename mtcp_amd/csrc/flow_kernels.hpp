@@ -65,31 +65,73 @@ struct PoolParams {
 // queue[g] for candidate g = i * kPorts + (port - MIN_PORT).  The reference
 // calls GetRSSCPUCore(daddr_h, saddr_h, dport_h, sport_h, ...)
 // (addr_pool.c:164): the peer's side comes first, as the incoming packets
-// of the connection will carry it.  Four candidates per lane, one dword store.
+// of the connection will carry it.
+//
+// The Toeplitz hash is linear over GF(2) (each input bit XORs a fixed
+// 32-bit window of the key into the hash, rss.c:63-79), so for the 96-bit
+// input daddr | saddr_i | dport | sport it splits into a part fixed per
+// address, C(i) (20 nibble tables), and a part of the port alone: the high
+// byte's two nibble tables (20, 21) and the low byte's (22, 23) merged into
+// two 256-entry byte tables.  And GetRSSCPUCore reads only the hash's low 7
+// bits ((h & 0x7F) [^ 3] % nq, rss.c:90-103), so every table holds just
+// those, and the queue of all 128 values is one more table.  A candidate then
+// costs three LDS byte reads (C(i) sits in a register) instead of 24 dword
+// reads and a division: bit-identical, by linearity.
+//
+// A workgroup maps one tile of kQmapTile consecutive candidates (at most two
+// addresses: kPorts > kQmapTile); each pass of its 256 lanes covers 1024
+// consecutive candidates, a lane four of them, so every dword store of a
+// wave is 256 contiguous bytes.
+constexpr uint32_t kQmapTile = 4 * 4 * kBlock;     // 4096 candidates per workgroup
+
+__device__ __forceinline__ uint32_t toeplitz_fixed7(const uint32_t *tab, uint32_t sip, uint32_t dip,
+                                                    uint32_t dport) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        h ^= tab[(t << 4) | ((sip >> (28 - 4 * t)) & 15u)];
+        h ^= tab[((8 + t) << 4) | ((dip >> (28 - 4 * t)) & 15u)];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) h ^= tab[((16 + t) << 4) | ((dport >> (12 - 4 * t)) & 15u)];
+    return h & 0x7Fu;
+}
+
 __global__ __launch_bounds__(kBlock) void rss_queue_map_kernel(PoolParams pp,
                                                                uint8_t *__restrict__ queue) {
-    __shared__ uint32_t tab[kRssTableWords];
-    for (int i = threadIdx.x; i < kRssTableWords; i += kBlock) tab[i] = pp.rss_tables[i];
+    __shared__ uint8_t t_hi[256], t_lo[256], q_of[128];
+    __shared__ uint32_t c_addr[2];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t *tab = pp.rss_tables;
+    const uint64_t first = (uint64_t)blockIdx.x * kQmapTile;
+    const uint32_t i0 = (uint32_t)(first / kPorts);
+    {
+        const uint32_t b = tid;                                    // kBlock == 256
+        t_hi[b] = (uint8_t)((tab[(20 << 4) | (b >> 4)] ^ tab[(21 << 4) | (b & 15u)]) & 0x7Fu);
+        t_lo[b] = (uint8_t)((tab[(22 << 4) | (b >> 4)] ^ tab[(23 << 4) | (b & 15u)]) & 0x7Fu);
+        if (b < 128) q_of[b] = (uint8_t)rss_core(b, pp.nq, pp.endian);
+        if (b < 2) c_addr[b] = toeplitz_fixed7(tab, pp.daddr_h, pp.saddr_base_h + i0 + b, pp.dport_h);
+    }
     __syncthreads();
-    const uint64_t quads = (pp.total + 3) / 4;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x; q < quads; q += stride) {
+    const uint64_t edge = (uint64_t)(i0 + 1) * kPorts;             // first candidate of address i0 + 1
+    const uint32_t c0 = c_addr[0], c1 = c_addr[1];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t g0 = first + 1024u * k + 4u * tid;
+        if (g0 >= pp.total) break;
         uint32_t word = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const uint64_t g = 4 * q + b;
-            if (g < pp.total) {
-                const uint32_t i = (uint32_t)(g / kPorts);
-                const uint32_t port = MTCP_GPU_MIN_PORT + (uint32_t)(g - (uint64_t)i * kPorts);
-                const uint32_t h = toeplitz96(tab, pp.daddr_h, pp.saddr_base_h + i,
-                                              (pp.dport_h << 16) | port);
-                word |= rss_core(h, pp.nq, pp.endian) << (8 * b);
-            }
+            const uint64_t g = g0 + b;
+            const bool second = g >= edge;
+            const uint32_t port = MTCP_GPU_MIN_PORT + (uint32_t)(g - (second ? edge : edge - kPorts));
+            const uint32_t m = (second ? c1 : c0) ^ t_hi[port >> 8] ^ t_lo[port & 0xFFu];
+            word |= (uint32_t)q_of[m] << (8 * b);
         }
-        if (4 * q + 3 < pp.total) {
-            reinterpret_cast<uint32_t *>(queue)[q] = word;
+        if (g0 + 3 < pp.total) {
+            reinterpret_cast<uint32_t *>(queue)[g0 / 4] = word;
         } else {
-            for (int b = 0; 4 * q + b < pp.total; ++b) queue[4 * q + b] = (uint8_t)(word >> (8 * b));
+            for (int b = 0; g0 + b < pp.total; ++b) queue[g0 + b] = (uint8_t)(word >> (8 * b));
         }
     }
 }

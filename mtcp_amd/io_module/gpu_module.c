@@ -687,6 +687,16 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
     return INNER_CALL(ctx, gpu_inner_module->dev_ioctl(ctx, nif, cmd, argp));
 }
 
+#ifdef MTCP_GPU_TESTING
+/* Test builds: the device a thread's context runs on, -1 when it passes
+ * through (the multi-device test checks the NUMA choice with it). */
+int gpu_module_thread_device(struct mtcp_thread_context *ctx)
+{
+    struct gpu_private_context *g = ctx->io_private_context;
+    return g && g->gpu ? g->slot_dev : -1;
+}
+#endif
+
 io_module_func gpu_module_func = {
     .load_module    = gpu_load_module,
     .init_handle    = gpu_init_handle,

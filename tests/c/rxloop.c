@@ -30,6 +30,9 @@
  *            may run on, as mtcp_core_affinitize (cpu.c) pins each mTCP
  *            thread to its core (RXLOOP_CPUS=a,b,..: thread t on the t-th
  *            CPU of that list; RXLOOP_PIN=0: unpinned)
+ *   RXLOOP_CTX_CPU=1 the thread's mtcp_thread_context.cpu is the cpu it is
+ *            pinned to (mTCP's ctx->cpu is the core, core.c:1057), not its
+ *            index: gpu_module.c then picks the GPU on that cpu's node
  *   RXLOOP_PASSES=p  (timing modes) each thread's backend serves its shard p
  *            times over, so that a run lasts long enough to time many threads
  *   RXLOOP_REF=lib   (timing modes) the software checks of a thread the module
@@ -65,6 +68,7 @@ uint16_t TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t d
 }
 
 extern io_module_func gpu_module_func;
+int gpu_module_thread_device(struct mtcp_thread_context *ctx);   /* test build of gpu_module.c */
 struct mtcp_config CONFIG = {1};                   /* one interface (mtcp.conf's port list) */
 extern io_module_func *gpu_inner_module;
 
@@ -174,6 +178,7 @@ struct worker {
     uint64_t rx_packets, rx_errors, changed, hdr_sum;
     int rounds, ioctl_ip, ioctl_tcp, ioctl_tx, sw_filled;
     uint32_t seen;
+    int device;                            /* gpu_module_thread_device after init */
     struct timespec t1;
 };
 static pthread_barrier_t g_start;
@@ -230,6 +235,7 @@ static void *worker_main(void *arg)
     w->ioctl_ip = w->ioctl_tcp = -2;
     gpu_module_func.init_handle(&ctx);
     gpu_module_func.link_devices(&ctx);
+    w->device = gpu_module_thread_device(&ctx);
     if (pthread_barrier_wait(&g_start) == PTHREAD_BARRIER_SERIAL_THREAD)
         clock_gettime(CLOCK_MONOTONIC, &g_t0);
     pthread_barrier_wait(&g_start);                  /* g_t0 set before anyone runs */
@@ -389,6 +395,8 @@ int main(int argc, char **argv)
         const uint32_t hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
         w->cpu = t;
         w->pin_cpu = pin_cpu[t];
+        if (getenv("RXLOOP_CTX_CPU") && strcmp(getenv("RXLOOP_CTX_CPU"), "1") == 0 && pin_cpu[t] >= 0)
+            w->cpu = pin_cpu[t];
         w->timing = timing;
         w->tx = tx;
         w->fake.tx_buf = tx_buf;
@@ -442,16 +450,20 @@ int main(int argc, char **argv)
     }
     if (!out || fwrite(status, 1, n, out) != n) { perror(argv[3]); return 1; }
     fclose(out);
+    char devs[64 * 12] = "", *dp = devs;
+    for (t = 0; t < threads; t++)
+        dp += sprintf(dp, "%s[%d, %d]", t ? ", " : "", ws[t].cpu, ws[t].device);
     secs = (double)(t1.tv_sec - g_t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - g_t0.tv_nsec);
     printf("{\"frames\": %u, \"seen\": %u, \"rounds\": %d, \"inner_bursts\": %d, "
            "\"rx_packets\": %llu, \"rx_errors\": %llu, \"changed\": %llu, "
            "\"ioctl_rx_ip\": %d, \"ioctl_rx_tcp\": %d, \"seconds\": %.6f, "
            "\"frame_bytes\": %llu, \"timing_mode\": %d, \"hdr_sum\": %llu, \"threads\": %d, "
-           "\"offloading_threads\": %d, \"passes\": %u, \"sw_checks\": \"%s\"}\n",
+           "\"offloading_threads\": %d, \"passes\": %u, \"sw_checks\": \"%s\", "
+           "\"cpu_device\": [%s]}\n",
            n, seen, rounds, recv_calls, (unsigned long long)rx_packets,
            (unsigned long long)rx_errors, (unsigned long long)changed, ws[0].ioctl_ip,
            ws[0].ioctl_tcp, secs, (unsigned long long)frame_bytes, timing,
-           (unsigned long long)hdr_sum, threads, offloading, passes, g_ref_rx ? "reference" : "oracle");
+           (unsigned long long)hdr_sum, threads, offloading, passes, g_ref_rx ? "reference" : "oracle", devs);
     free(ws);
     free(status);
     free((void *)buf);

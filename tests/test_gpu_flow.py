@@ -119,3 +119,29 @@ def test_rss_queue_map_vs_oracle(gpu):
         i, port = divmod(int(g), 64511)
         want = oracle.rss_cpu_core(cache, daddr_h, base_h + i, dport_h, 1025 + port, nq, 1)
         assert got[g] == want, (i, port)
+
+
+@pytest.mark.parametrize("key_name,num_addr,nq,endian", [("0x05", 3, 5, 1), ("microsoft", 3, 16, 0),
+                                                         ("microsoft", 2, 3, 1), ("0x05", 1, 1, 0)])
+def test_rss_queue_map_every_candidate(gpu, key_name, num_addr, nq, endian):
+    """The queue map (the split Toeplitz: a per-address part and two port-byte
+    tables, flow_kernels.hpp) equals GetRSSCPUCore (rss.c:90-103, the oracle)
+    on EVERY candidate, across address edges inside a workgroup's tile and
+    the batch's ragged end; nothing written past the candidates."""
+    key = oracle.KEY_0X05 if key_name == "0x05" else oracle.KEY_MICROSOFT
+    base_h, daddr_h, dport_h = 0xC0A80A01, 0x0A000005, 8080
+    total = num_addr * 64511
+    q = torch.full((total + 64,), 0xAA, dtype=torch.uint8, device=DEV)
+    cache = oracle.key_cache(key)
+    with gpu.Context(rss_key=key) as ctx:
+        ctx.rss_queue_map_dev(base_h, num_addr, daddr_h, dport_h, nq, bool(endian), q)
+        ctx.sync()
+    got = q.cpu().numpy()
+    assert (got[total:] == 0xAA).all()
+    want = np.empty(total, np.uint8)
+    for i in range(num_addr):
+        for port in range(64511):
+            want[i * 64511 + port] = oracle.rss_cpu_core(cache, daddr_h, base_h + i, dport_h, 1025 + port,
+                                                         nq, endian)
+    bad = np.nonzero(got[:total] != want)[0]
+    assert len(bad) == 0, (len(bad), bad[:10])

@@ -105,3 +105,48 @@ def test_split_cpus_edge_cases(tmp_path):
     assert [shard.split_cpus({0, 1}, i, 4, str(tmp_path)) for i in range(4)] == [{0}, {1}, {0}, {1}]
     # no topology in sysfs: every cpu is its own core
     assert shard.split_cpus({5, 6, 7, 8}, 1, 2, str(tmp_path / "none")) == {7, 8}
+
+
+def _cpu_baseline_worker(rank, world, port, q):
+    """One bench.py rank's N > 1 CPU-baseline leg on the CPU: its shard of a
+    C4-shaped batch in host memory, the reference's rx code (or the oracle)
+    on its share of the cores, all ranks at once."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    os.sched_setaffinity(0, shard.split_cpus(os.sched_getaffinity(0), rank, world))
+    s = shard.make_shard(4096 * world, 1500, rank, world, 4)
+    buf = np.zeros(s.nbytes, np.uint8)
+    oracle.pktgen(buf, s.desc, 6, 4, s.first_index)
+    r = bench.cpu_baseline_ranks(buf, s.desc, bench.CONFIGS["c4"], 2048, world, rank)
+    if rank == 0:
+        q.put(r)
+    else:
+        assert r is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_cpu_baseline_at_n_ranks():
+    """bench.py's CPU baseline at N > 1: every rank
+    times its own shard at once; rank 0 reports each rank and the host
+    aggregate (all sample bytes / the slowest rank's time), with cores."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000) + 101
+    procs = [ctx.Process(target=_cpu_baseline_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    r = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert r["kind"] in ("reference", "port") and r["unit"] == "GB/s"
+    assert [x["rank"] for x in r["per_rank"]] == [0, 1]
+    assert r["cores"] == sum(x["cores"] for x in r["per_rank"]) >= 2
+    slowest = max(x["seconds"] for x in r["per_rank"])
+    assert abs(r["value"] - 2 * 2048 * 1500 / slowest / 1e9) < 0.01 * r["value"]   # seconds rounded to 1 us
+    assert r["value"] <= sum(x["GB/s"] for x in r["per_rank"]) + 1e-3
