@@ -729,6 +729,25 @@ def main():
     ctx = gpu.Context(device, rss=cfg["rss"], rss_queues=8, rss_endian=True, compact=compact)
     step = lambda: ctx.rx_chunk_dev(d_buf, d_desc, sh.count, 6, d_out, stream=stream)
 
+    ceiling = None
+    if args.ceiling == "on":
+        # The box's read ceiling on this rank's own frame buffer, measured
+        # right before the kernel so that both see the same device state
+        # (a cold device runs its first launches a few us slow: C2 at
+        # --steps 20 --warmup 5 averaged 243 us after nothing, 239 us after
+        # 200 launches).  Every rank times its own GPU; the slowest GPU's
+        # stream is the ceiling the slowest rank's launches (kern_ms_max)
+        # are compared with.
+        try:
+            ceiling = read_ceiling(d_buf, sh.nbytes, stream)
+        except Exception as exc:   # never costs the headline line
+            ceiling = repr(exc)
+        if world > 1:
+            t = torch.tensor([ceiling[0] if isinstance(ceiling, tuple) else -1.0], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if isinstance(ceiling, tuple):
+                ceiling = (float(t[0]), ceiling[1])
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -785,19 +804,6 @@ def main():
         kern_ms_max = kern_ms
 
     kernel = ctx.last_kernel                 # the kernel the timed launches dispatched
-    ceiling = None
-    if args.ceiling == "on":
-        # every rank times its own GPU; the slowest GPU's stream is the ceiling
-        # the slowest rank's launches (kern_ms_max) are compared with
-        try:
-            ceiling = read_ceiling(d_buf, sh.nbytes, stream)
-        except Exception as exc:   # never costs the headline line
-            ceiling = repr(exc)
-        if world > 1:
-            t = torch.tensor([ceiling[0] if isinstance(ceiling, tuple) else -1.0], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            if isinstance(ceiling, tuple):
-                ceiling = (float(t[0]), ceiling[1])
     # verdict summary of the last step (sanity: corruption rate ~1/1024 + 1/4096)
     recs = d_out.view(-1, rec_bytes)
     v_at, pl_at = (14, 8) if compact else (36, 32)   # verdict, payload_len (include/mtcp_gpu.h)

@@ -451,19 +451,25 @@ int main(int argc, char **argv)
     if (!out || fwrite(status, 1, n, out) != n) { perror(argv[3]); return 1; }
     fclose(out);
     char devs[64 * 12] = "", *dp = devs;
-    for (t = 0; t < threads; t++)
+    char tsec[64 * 24] = "", *tp = tsec;
+    for (t = 0; t < threads; t++) {
         dp += sprintf(dp, "%s[%d, %d]", t ? ", " : "", ws[t].cpu, ws[t].device);
+        /* each thread's own time from the common start, and whether it offloaded */
+        tp += sprintf(tp, "%s[%.6f, %d]", t ? ", " : "",
+                      (double)(ws[t].t1.tv_sec - g_t0.tv_sec) + 1e-9 * (double)(ws[t].t1.tv_nsec - g_t0.tv_nsec),
+                      ws[t].ioctl_tcp == 0);
+    }
     secs = (double)(t1.tv_sec - g_t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - g_t0.tv_nsec);
     printf("{\"frames\": %u, \"seen\": %u, \"rounds\": %d, \"inner_bursts\": %d, "
            "\"rx_packets\": %llu, \"rx_errors\": %llu, \"changed\": %llu, "
            "\"ioctl_rx_ip\": %d, \"ioctl_rx_tcp\": %d, \"seconds\": %.6f, "
            "\"frame_bytes\": %llu, \"timing_mode\": %d, \"hdr_sum\": %llu, \"threads\": %d, "
            "\"offloading_threads\": %d, \"passes\": %u, \"sw_checks\": \"%s\", "
-           "\"cpu_device\": [%s]}\n",
+           "\"cpu_device\": [%s], \"thread_seconds_offload\": [%s]}\n",
            n, seen, rounds, recv_calls, (unsigned long long)rx_packets,
            (unsigned long long)rx_errors, (unsigned long long)changed, ws[0].ioctl_ip,
            ws[0].ioctl_tcp, secs, (unsigned long long)frame_bytes, timing,
-           (unsigned long long)hdr_sum, threads, offloading, passes, g_ref_rx ? "reference" : "oracle", devs);
+           (unsigned long long)hdr_sum, threads, offloading, passes, g_ref_rx ? "reference" : "oracle", devs, tsec);
     free(ws);
     free(status);
     free((void *)buf);

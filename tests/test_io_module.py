@@ -162,7 +162,8 @@ def test_gpu_threads_limit_splits_the_checks(tmp_path, golden, limit):
         os.environ.pop("MTCP_GPU_THREADS", None)
     stats, status = run_rxloop(tmp_path, threads=4, mode="timing", env=env)
     drop = rx_drops(golden)
-    assert stats["offloading_threads"] == {None: 2, "all": 4}.get(limit, limit and int(limit))
+    want = {None: 2, "all": 4}[limit] if limit in (None, "all") else int(limit)
+    assert stats["offloading_threads"] == want
     assert stats["seen"] == stats["frames"] == len(golden.desc)
     assert np.array_equal(status == 0, drop)
     assert stats["rx_errors"] == int(drop.sum())

@@ -130,6 +130,7 @@ def run(n, size, seed, tmp, mode, threads=1, pipeline=True, tx=True, reps=3):
             "bursts_per_launch": 64, "burst": 64, "seconds": s,
             "mpkt_per_s": round(n / s / 1e6, 3), "GBs": round(best["frame_bytes"] / s / 1e9, 3),
             "rx_errors": best["rx_errors"], "changed": best["changed"],
+            "thread_seconds_offload": best.get("thread_seconds_offload"),
             "ioctl_rx_tcp": best["ioctl_rx_tcp"],
             "note": "each mTCP thread: copy into pinned staging + one H2D (frames + descriptors) + "
                     "rx kernel + D2H per 4096 frames, get_rptr from staging; pipelined: aggregate "
@@ -202,6 +203,52 @@ def main():
                 os.sched_setaffinity(0, local)
                 try:
                     ref = reference(n, size, seed, (1, 4, 8, 16))
+                finally:
+                    os.sched_setaffinity(0, saved)
+                if ref:
+                    ref["pinned"] = "gpu_local_cpus"
+                    print(json.dumps(ref), flush=True)
+        return
+    if "--admission" in sys.argv:
+        # The default admission (two offloading threads per GPU) against no
+        # offload and every thread offloading, interleaved reps; each line
+        # carries every thread's own rate, split into offloading and
+        # software threads, so that the slowest-thread bound is visible.
+        # Software threads run the reference's own chain (RXLOOP_REF).
+        import oracle
+        host = host_topology()
+        print(json.dumps(host), flush=True)
+        local = host["gpu_local_cpus"]
+        saved = os.sched_getaffinity(0)
+        if oracle.ref_available():
+            os.environ["RXLOOP_REF"] = oracle.REF_LIB_PATH
+        reps = int(os.environ.get("ADMISSION_REPS", "4"))
+        with tempfile.TemporaryDirectory() as tmp:
+            for size, seed, tlist in ((1500, 2, (1, 2, 4, 8, 16)), (64, 1, (4, 16))):
+                for rep in range(reps):
+                    for threads in tlist:
+                        for limit in ("default", "0", "all"):
+                            os.environ["RXLOOP_CPUS"] = ",".join(map(str, local))
+                            os.environ["RXLOOP_PASSES"] = str(max(4, 4 * threads) if size == 1500 else 2 * threads)
+                            os.environ.pop("MTCP_GPU_THREADS", None)
+                            if limit != "default":
+                                os.environ["MTCP_GPU_THREADS"] = limit
+                            r = run(n, size, seed, tmp, "timing", threads, True, reps=1)
+                            per = r["thread_seconds_offload"] or []
+                            share = r["frames"] / max(threads, 1)
+                            off = [share / s / 1e6 for s, o in per if o]
+                            sw = [share / s / 1e6 for s, o in per if not o]
+                            print(json.dumps({"probe": "io_admission", "rep": rep, "frame_size": size,
+                                              "threads": threads, "gpu_threads": limit,
+                                              "offloading_threads": r["offloading_threads"],
+                                              "mpkt_per_s": r["mpkt_per_s"], "GBs": r["GBs"],
+                                              "offload_thread_mpps": [round(x, 2) for x in off],
+                                              "sw_thread_mpps": [round(x, 2) for x in sw]}), flush=True)
+                for k in ("MTCP_GPU_THREADS", "RXLOOP_CPUS", "RXLOOP_PASSES"):
+                    os.environ.pop(k, None)
+                os.sched_setaffinity(0, local)
+                try:
+                    ref = reference(n, size, seed, tlist)
                 finally:
                     os.sched_setaffinity(0, saved)
                 if ref:

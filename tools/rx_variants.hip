@@ -609,8 +609,17 @@ int main(int argc, char **argv) {
     std::vector<Variant> vs;
     using namespace mg;
     if (rss) {
-        // variant 0 = what mtcp_gpu.hip dispatches for C3; every other variant's
-        // records must equal its records byte for byte
+        // variant 0 = what mtcp_gpu.hip dispatches for C3 (sorted, runs of 16);
+        // every other variant's records must equal its records byte for byte
+        vs.push_back({"b16_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16>, 2});
+        // the read ceiling's shapes on this buffer (tools/stream_ceiling.hip)
+        vs.push_back({"plain_ceil3_cu2", plain_ceil<3>, 2});
+        vs.push_back({"plain_ceil4_cu2", plain_ceil<4>, 2});
+        vs.push_back({"plain_ceil6_cu2", plain_ceil<6>, 2});
+        vs.push_back({"plain_ceil8_cu4", plain_ceil<8>, 4});
+        // the ladder of the shipped schedule: phase 1 alone, + records
+        vs.push_back({"abl1_b16_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 16>, 2});
+        vs.push_back({"abl1_b16_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 8, 16>, 2});
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
         vs.push_back({"rss_sorted6_wpb8_cu1", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 8>, 1, 8});
         vs.push_back({"rss_sorted6_wpb2_cu4", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 2>, 4, 2});
@@ -649,7 +658,6 @@ int main(int argc, char **argv) {
         vs.push_back({"runstream16skip_cu2", run_stream<16, true>, 2});
         vs.push_back({"runstream24skip_cu2", run_stream<24, true>, 2});
 
-        vs.push_back({"b16_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16>, 2});
         vs.push_back({"b32_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 32>, 2});
         vs.push_back({"abl1_rss_sorted6_nostore_u8_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 8, true, 8>, 2});
         vs.push_back({"rss_sorted6_u8_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 8>, 2});
