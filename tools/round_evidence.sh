@@ -27,5 +27,7 @@ bash tools/gpu_steps.sh \
   "bf1|150|python bench.py --config f1" \
   "bf3|150|python bench.py --config f3" \
   "bf4|150|python bench.py --config f4" \
+  "c2x5|300|for i in 1 2 3 4 5; do python bench.py --steps 20 --warmup 5 --cpu-baseline off --pcie off --small-batch off || exit 1; done" \
+  "bn2|200|MTCP_BENCH_DEVICE=0 python bench.py --gpus 2 --steps 20 --warmup 5 --pcie off" \
   "pr|240|bash tools/profile_rows.sh gpurun_out/prof_rows" \
   "wp|120|./tools/wave_probe 1500 64 1024 4096 16384 32768 && ./tools/wave_probe 9000 64 4096 16384 && ./tools/wave_probe 64 64 4096 16384 65536"
