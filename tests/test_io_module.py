@@ -251,12 +251,15 @@ def test_host_code_under_address_sanitizer(tmp_path, golden):
     exe = tmp_path / "rxloop_asan"
     cmd = ["gcc", "-std=gnu99", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
            "-fno-sanitize-recover=undefined", "-Wall", "-pthread",
-           "-I" + os.path.join(ROOT, "tests", "c", "mtcp_double"), "-I" + os.path.join(ROOT, "include"),
+           "-DMTCP_GPU_TESTING",           # rxloop is a test harness: the test build of the module
+           "-I" + os.path.join(ROOT, "tests", "c", "mtcp_double"), "-I" + os.path.join(ROOT, "tests", "c"),
+           "-I" + os.path.join(ROOT, "include"),
            "-o", str(exe), os.path.join(ROOT, "tests", "c", "rxloop.c"),
            os.path.join(ROOT, "mtcp_amd", "io_module", "gpu_module.c"),
            os.path.join(ROOT, "oracle", "mtcp_oracle.c"),
-           "-L" + os.path.join(ROOT, "mtcp_amd", "lib"), "-lmtcp_gpu",
-           "-Wl,-rpath," + os.path.join(ROOT, "mtcp_amd", "lib")]
+           "-L" + os.path.join(ROOT, "mtcp_amd", "lib"), "-L" + os.path.join(ROOT, "tests", "c"),
+           "-lmtcp_gpu", "-lmtcp_gpu_testing", "-ldl",
+           "-Wl,-rpath," + os.path.join(ROOT, "mtcp_amd", "lib"), "-Wl,-rpath," + os.path.join(ROOT, "tests", "c")]
     p = subprocess.run(cmd, capture_output=True, text=True)
     if p.returncode != 0 and "asan" in p.stderr.lower():
         pytest.skip("no ASan runtime: " + p.stderr[-200:])
