@@ -621,6 +621,11 @@ int main(int argc, char **argv) {
         vs.push_back({"abl1_b16_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 16>, 2});
         vs.push_back({"abl1_b16_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 8, 16>, 2});
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
+        // round 4: three large rounds in flight
+        vs.push_back({"abl1_b16_rss_sorted6_nostore_nb3_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 16, true, 6, false, false, 0, 4, 0, false, 2, true, 3>, 2});
+        vs.push_back({"b16_rss_sorted6_nb3_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, false, 2, true, 3>, 2});
+        vs.push_back({"b16_rss_sorted6_cmp_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, true>, 2});
+        vs.push_back({"b16_rss_sorted6_cmp_nb3_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, true, 2, true, 3>, 2});
         vs.push_back({"rss_sorted6_wpb8_cu1", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 8>, 1, 8});
         vs.push_back({"rss_sorted6_wpb2_cu4", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 2>, 4, 2});
         vs.push_back({"rss_sorted6_prio1half_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 5>, 2});
@@ -771,6 +776,7 @@ int main(int argc, char **argv) {
     std::vector<std::vector<float>> ms(vs.size());
     // the ABL 1 records (chunk sums), which the one-wave-per-packet variants must equal
     std::vector<mtcp_gpu_result> abl1_rec;
+    std::vector<uint8_t> cmp_rec;                   // the first compact variant's 16 B records
     const int reps = 20;
     for (int r = 0; r < rounds; ++r) {
         for (size_t v = 0; v < vs.size(); ++v) {
@@ -802,7 +808,17 @@ int main(int argc, char **argv) {
                     return 2;
                 }
             }
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "wpp") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && !strstr(vs[v].name, "runstream")) {
+            // compact-record (CMP) variants: 16 B records, compared among themselves
+            if (r == 0 && strstr(vs[v].name, "_cmp")) {
+                std::vector<uint8_t> y(n * 16);
+                CK(hipMemcpy(y.data(), d_out, n * 16, hipMemcpyDeviceToHost));
+                if (cmp_rec.empty()) cmp_rec = y;
+                else if (memcmp(cmp_rec.data(), y.data(), n * 16) != 0) {
+                    fprintf(stderr, "variant %s differs from the first compact variant\n", vs[v].name);
+                    return 2;
+                }
+            }
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "wpp") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && !strstr(vs[v].name, "runstream") && !strstr(vs[v].name, "_cmp")) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
