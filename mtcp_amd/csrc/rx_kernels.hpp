@@ -714,11 +714,9 @@ struct Trip {
 // VGPRs; 3: 168, a third workgroup per CU; tools/occ_probe.hip).
 // COOP: the workgroup loads its descriptors together (phase 0 below; the
 // unrolled schedule of the chunk modes); false: each lane its own (A/B).
-// NB (size-sorted schedules): large rounds in flight, 2 (X/Y) or 3 (X/Y/Z).
 template <int MODE, bool RSS, int SCHED, bool LALIGN = false, int ABL = 0, int DEFER = 8, int B = 8,
           bool NT = true, int U = 6, bool REV = false, bool STAMP = false, int PRIO = 0,
-          int WPB = kWavesPerBlock, int XSKIP = 0, bool CMP = false, int WPE = 2, bool COOP = true,
-          int NB = 2>
+          int WPB = kWavesPerBlock, int XSKIP = 0, bool CMP = false, int WPE = 2, bool COOP = true>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE))) void rx_kernel(KParams kp) {
 #ifndef MTCP_GPU_TESTING
     // the product library instantiates no profiling or timing-probe variant
@@ -1189,41 +1187,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(WPE
                 }
                 have_pre_small = false;
             }
-            if (NB == 3 && RL > 0) {   // (NB is a template constant)
-                // three large rounds in flight: round i + 2 goes out before
-                // round i is consumed
-                v4u Z3[U];
-                Trip ta, tb, tc;
-                if (have_pre) {
-                    ta = pre;
-                } else {
-                    big_trip(nL, 0, ta);
-                    issue(ta, X);
-                }
-                if (RL > 1) {
-                    big_trip(nL, 1, tb);
-                    issue(tb, Y);
-                }
-                for (uint32_t i = 0; i < RL; i += 3) {
-                    if (i + 2 < RL) {
-                        big_trip(nL, i + 2, tc);
-                        issue(tc, Z3);
-                    }
-                    finish_big(ta, X);
-                    if (i + 1 >= RL) break;
-                    if (i + 3 < RL) {
-                        big_trip(nL, i + 3, ta);
-                        issue(ta, X);
-                    }
-                    finish_big(tb, Y);
-                    if (i + 2 >= RL) break;
-                    if (i + 4 < RL) {
-                        big_trip(nL, i + 4, tb);
-                        issue(tb, Y);
-                    }
-                    finish_big(tc, Z3);
-                }
-            } else if (RL > 0) {
+            if (RL > 0) {
                 Trip cur, nxt;
                 if (have_pre) {
                     cur = pre;

@@ -621,11 +621,7 @@ int main(int argc, char **argv) {
         vs.push_back({"abl1_b16_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 16>, 2});
         vs.push_back({"abl1_b16_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 8, 16>, 2});
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
-        // round 4: three large rounds in flight
-        vs.push_back({"abl1_b16_rss_sorted6_nostore_nb3_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 16, true, 6, false, false, 0, 4, 0, false, 2, true, 3>, 2});
-        vs.push_back({"b16_rss_sorted6_nb3_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, false, 2, true, 3>, 2});
         vs.push_back({"b16_rss_sorted6_cmp_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, true>, 2});
-        vs.push_back({"b16_rss_sorted6_cmp_nb3_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, true, 2, true, 3>, 2});
         vs.push_back({"rss_sorted6_wpb8_cu1", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 8>, 1, 8});
         vs.push_back({"rss_sorted6_wpb2_cu4", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 2>, 4, 2});
         vs.push_back({"rss_sorted6_prio1half_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 5>, 2});
