@@ -344,16 +344,23 @@ def cpu_baseline_ranks(host_buf, desc, cfg, sample_n, world, rank):
     cores = cpu_share()
     kind = "reference" if oracle.ref_available() else "port"
     dist.barrier()
-    if kind == "reference":
-        best = oracle.ref_bench_rx(buf, d, 6, cfg["rss"], cores, 5)
-    else:
-        best = oracle.bench_rx(buf, d, 6, oracle.rss_cfg(None, 8, 1) if cfg["rss"] else None, cores, 5)
+    try:
+        if kind == "reference":
+            best = oracle.ref_bench_rx(buf, d, 6, cfg["rss"], cores, 5)
+        else:
+            best = oracle.bench_rx(buf, d, 6, oracle.rss_cfg(None, 8, 1) if cfg["rss"] else None, cores, 5)
+    except Exception as exc:   # every rank still joins the gather below: no hang
+        print(f"bench.py rank {rank}: cpu baseline failed: {exc!r}", file=sys.stderr)
+        best = -1.0
     mine = torch.tensor([nbytes, n, best, cores, float(ord(kind[0]))], dtype=torch.float64)
     rows = [torch.zeros(5, dtype=torch.float64) for _ in range(world)]
     dist.all_gather(rows, mine)
     if rank != 0:
         return None
     rows = [r.tolist() for r in rows]
+    failed = [i for i, r in enumerate(rows) if r[2] <= 0]
+    if failed:
+        return {"value": None, "error": f"the CPU baseline failed on ranks {failed} (their stderr says why)"}
     kinds = {"reference" if int(r[4]) == ord("r") else "port" for r in rows}
     total_bytes = sum(r[0] for r in rows)
     total_pkts = sum(r[1] for r in rows)
@@ -727,7 +734,17 @@ def main():
     frame_bytes = int(sh.desc["len"].astype(np.int64).sum())
 
     ctx = gpu.Context(device, rss=cfg["rss"], rss_queues=8, rss_endian=True, compact=compact)
-    step = lambda: ctx.rx_chunk_dev(d_buf, d_desc, sh.count, 6, d_out, stream=stream)
+    # One step = one mtcp_gpu_rx_chunk_dev call, issued as a C caller would:
+    # the C-ABI function with its arguments bound once (the Python wrapper's
+    # per-call argument handling, ~5-10 us, is otherwise on the critical path
+    # of the first timed launch); every return code is checked after the
+    # timed region.
+    from mtcp_amd import _lib
+    rx_fn = _lib.lib().mtcp_gpu_rx_chunk_dev
+    rx_args = (ctx._h, d_buf.data_ptr(), sh.nbytes, d_desc.data_ptr(), sh.count, 6, d_out.data_ptr(),
+               stream.cuda_stream)
+    step_rcs = []
+    step = lambda: step_rcs.append(rx_fn(*rx_args))
 
     ceiling = None
     if args.ceiling == "on":
@@ -803,6 +820,9 @@ def main():
     else:
         kern_ms_max = kern_ms
 
+    bad = [rc for rc in step_rcs if rc != 0]
+    if bad:
+        raise SystemExit(f"bench.py: mtcp_gpu_rx_chunk_dev failed in the timed steps ({bad[0]})")
     kernel = ctx.last_kernel                 # the kernel the timed launches dispatched
     # verdict summary of the last step (sanity: corruption rate ~1/1024 + 1/4096)
     recs = d_out.view(-1, rec_bytes)
@@ -843,7 +863,7 @@ def main():
             except Exception as exc:   # report, never fake
                 extra["cpu_baseline"] = {"value": None, "error": repr(exc)}
         else:
-            cb = cpu_baseline_ranks(host, hdesc, cfg, args.cpu_sample, world, rank)
+            cb = cpu_baseline_ranks(host, hdesc, cfg, args.cpu_sample, world, rank)   # collective
             if rank == 0:
                 extra["cpu_baseline"] = cb
         del host
