@@ -419,6 +419,92 @@ __global__ __launch_bounds__(256) void run_stream(mg::KParams kp) {
     if (acc == 0x12345678u) kp.out[0].saddr = acc;
 }
 
+namespace mg {
+// Probe (round 4): run_stream's linear walk of each run of 8 consecutive
+// frames, staged through an LDS image of the run (unconditional clamped
+// loads, so the 12 loads of a run stay in flight), then the per-frame sums
+// read back from LDS by 16-lane rows (frames of <= 96 chunks: C2, C3); the
+// loads of run j + 1 are in flight while run j is summed.  Timing only: sums
+// to out[k].saddr, no parse, no records (compare with abl1_*_nostore).
+template <int U>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void lds_run_walk(mg::KParams kp) {
+    __shared__ mg::v4u img[4][U * 64];
+    const uint32_t lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+    const uint32_t row = lane >> 4, rlane = lane & 15;
+    const uint32_t wave = blockIdx.x * 4 + wib, nw = gridDim.x * 4;
+    const uint64_t base = (uint64_t)(uintptr_t)kp.buf;
+    v4u *im = img[wib];
+    for (uint32_t g0 = 0; g0 < kp.n; g0 += nw * 64) {
+        const uint32_t k = g0 + (lane / 8) * (nw * 8) + wave * 8 + (lane % 8);
+        uint64_t lo = 0, hi = 0;
+        uint32_t nch = 0;
+        if (k < kp.n) {
+            const uint64_t raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
+            const uint64_t p = base + ((uint64_t)(uint32_t)raw << kp.off_shift);
+            const uint32_t L = (uint32_t)(raw >> 32) & 0xFFFFu;
+            lo = p & ~15ull;
+            hi = (p + L + 15) & ~15ull;
+            nch = L ? (uint32_t)((hi - lo) >> 4) : 0u;
+        }
+        auto run_lo = [&](int j) -> uint64_t {
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(lo >> 32), 8 * j) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lo, 8 * j);
+        };
+        auto run_nc = [&](int j) -> uint32_t {
+            const uint64_t rlo = run_lo(j);
+            const uint64_t rhi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hi >> 32), 8 * j + 7) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hi, 8 * j + 7);
+            return rlo == 0 || rhi <= rlo ? 0u : (uint32_t)((rhi - rlo) >> 4);
+        };
+        v4u x[U];
+        auto issue = [&](int j) {
+            const uint64_t rlo = run_lo(j);
+            const uint32_t nc = run_nc(j);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = u * 64 + lane;
+                x[u] = gload_nt(rlo + 16ull * (c < nc ? c : (nc ? nc - 1 : 0u)));   // clamp: no exec mask
+            }
+        };
+        issue(0);
+#pragma unroll 1
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t nc = run_nc(j);
+            const uint64_t rlo = run_lo(j);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                im[u * 64 + lane] = x[u];
+            __builtin_amdgcn_wave_barrier();
+            if (j + 1 < 8) issue(j + 1);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int src = 8 * j + 4 * h + (int)row;
+                const uint32_t f_n = shfl32(nch, src);
+                const uint32_t f_lo = shfl32((uint32_t)lo, src);
+                const uint32_t s = (f_lo - (uint32_t)rlo) >> 4;
+                uint32_t acc = 0;
+                v4u y[6];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    const uint32_t c = u * 16 + rlane;
+                    y[u] = im[(s + (c < f_n ? c : 0u)) & (U * 64 - 1 > 0 ? 0xFFFFFFFFu : 0u)];
+                }
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    const uint32_t c = u * 16 + rlane;
+                    const uint32_t v = halves4(y[u], 0u);
+                    acc += c < f_n ? v : 0u;
+                }
+                acc = row_sum(acc);
+                const uint32_t kk = g0 + j * (nw * 8) + wave * 8 + 4 * h + row;
+                if (rlane == 15 && kk < kp.n) kp.out[kk].saddr = acc;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+}  // namespace mg
+
 struct Variant { const char *name; kfn fn; uint32_t blocks_per_cu; uint32_t wpb = 4; };
 
 static uint64_t mix(uint64_t z) {
@@ -622,6 +708,7 @@ int main(int argc, char **argv) {
         vs.push_back({"abl1_b16_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 8, 16>, 2});
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
         vs.push_back({"b16_rss_sorted6_cmp_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, true>, 2});
+        vs.push_back({"ldsrun12_cu2", lds_run_walk<12>, 2});
         vs.push_back({"rss_sorted6_wpb8_cu1", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 8>, 1, 8});
         vs.push_back({"rss_sorted6_wpb2_cu4", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 2>, 4, 2});
         vs.push_back({"rss_sorted6_prio1half_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 5>, 2});
@@ -753,6 +840,7 @@ int main(int argc, char **argv) {
         vs.push_back({"runstream4_cu2", run_stream<4>, 2});
         vs.push_back({"runstream8_cu2", run_stream<8>, 2});
         vs.push_back({"runstream12_cu2", run_stream<12>, 2});
+        vs.push_back({"ldsrun12_cu2", lds_run_walk<12>, 2});
         // tx fill last: it repairs the corrupted frames the rx variants compare on
         vs.push_back({"tx_unrolled_cu2", rx_kernel<kTxChunk, false, 3>, 2});
         vs.push_back({"tx_unrolled_nodefer_cu2", rx_kernel<kTxChunk, false, 3, false, 0, 0>, 2});
@@ -814,7 +902,7 @@ int main(int argc, char **argv) {
                     return 2;
                 }
             }
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "wpp") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && !strstr(vs[v].name, "runstream") && !strstr(vs[v].name, "_cmp")) {
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "wpp") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && !strstr(vs[v].name, "runstream") && !strstr(vs[v].name, "ldsrun") && !strstr(vs[v].name, "_cmp")) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
