@@ -893,8 +893,10 @@ int mtcp_gpu_rss_queue_map_dev(mtcp_gpu_ctx *ctx, uint32_t saddr_base_h, uint32_
     pp.nq = (uint32_t)num_queues;
     pp.endian = endian_check ? 1u : 0u;
     pp.total = (uint64_t)num_addr * mg::kPorts;
-    // one tile of kQmapTile candidates per workgroup (at most 2^31 * 64511 / 4096 of them)
-    const uint32_t blocks = (uint32_t)((pp.total + mg::kQmapTile - 1) / mg::kQmapTile);
+    // one tile of kQmapTile candidates per workgroup, up to 8 workgroups per
+    // CU (the kernel walks further tiles grid-stride)
+    const uint64_t tiles = (pp.total + mg::kQmapTile - 1) / mg::kQmapTile;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)ctx->num_cu * 8);
     hipLaunchKernelGGL(mg::rss_queue_map_kernel, dim3(blocks), dim3(mg::kBlock), 0,
                        pick(ctx, stream), pp, d_queue);
     return HIP_OK(hipGetLastError()) ? MTCP_GPU_OK : MTCP_GPU_EIO;
