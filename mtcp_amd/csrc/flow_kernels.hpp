@@ -103,21 +103,21 @@ __global__ __launch_bounds__(kBlock) void rss_queue_map_kernel(PoolParams pp,
     __shared__ uint32_t c_addr[2];
     const uint32_t tid = threadIdx.x;
     const uint32_t *tab = pp.rss_tables;
+    // tiles of kQmapTile candidates, grid-stride (any num_addr: a grid of
+    // one workgroup per tile would pass 2^31 tiles at ~140 K addresses)
+    const uint64_t ntiles = (pp.total + kQmapTile - 1) / kQmapTile;
+    uint64_t tile = blockIdx.x;
+    uint64_t first = tile * kQmapTile;
+    uint32_t i0 = (uint32_t)(first / kPorts);
     {
         const uint32_t b = tid;                                    // kBlock == 256
         t_hi[b] = (uint8_t)((tab[(20 << 4) | (b >> 4)] ^ tab[(21 << 4) | (b & 15u)]) & 0x7Fu);
         t_lo[b] = (uint8_t)((tab[(22 << 4) | (b >> 4)] ^ tab[(23 << 4) | (b & 15u)]) & 0x7Fu);
         if (b < 128) q_of[b] = (uint8_t)rss_core(b, pp.nq, pp.endian);
+        if (b < 2) c_addr[b] = toeplitz_fixed7(tab, pp.daddr_h, pp.saddr_base_h + i0 + b, pp.dport_h);
     }
-    // tiles of kQmapTile candidates, grid-stride (any num_addr: a grid of
-    // one workgroup per tile would pass 2^31 tiles at ~140 K addresses)
-    const uint64_t ntiles = (pp.total + kQmapTile - 1) / kQmapTile;
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t first = tile * kQmapTile;
-    const uint32_t i0 = (uint32_t)(first / kPorts);
-    __syncthreads();                                               // the last tile's c_addr is read
-    if (tid < 2) c_addr[tid] = toeplitz_fixed7(tab, pp.daddr_h, pp.saddr_base_h + i0 + tid, pp.dport_h);
     __syncthreads();
+    for (;;) {
     const uint64_t edge = (uint64_t)(i0 + 1) * kPorts;             // first candidate of address i0 + 1
     const uint32_t c0 = c_addr[0], c1 = c_addr[1];
 #pragma unroll
@@ -139,6 +139,13 @@ __global__ __launch_bounds__(kBlock) void rss_queue_map_kernel(PoolParams pp,
             for (int b = 0; g0 + b < pp.total; ++b) queue[g0 + b] = (uint8_t)(word >> (8 * b));
         }
     }
+    tile += gridDim.x;                                             // the next tile, if any
+    if (tile >= ntiles) break;
+    first = tile * kQmapTile;
+    i0 = (uint32_t)(first / kPorts);
+    __syncthreads();                                               // this tile's c_addr is read
+    if (tid < 2) c_addr[tid] = toeplitz_fixed7(tab, pp.daddr_h, pp.saddr_base_h + i0 + tid, pp.dport_h);
+    __syncthreads();
     }
 }
 

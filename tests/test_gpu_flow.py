@@ -145,3 +145,28 @@ def test_rss_queue_map_every_candidate(gpu, key_name, num_addr, nq, endian):
                                                          nq, endian)
     bad = np.nonzero(got[:total] != want)[0]
     assert len(bad) == 0, (len(bad), bad[:10])
+
+
+def test_rss_queue_map_more_tiles_than_the_grid(gpu):
+    """200 addresses = 12.9 M candidates = 3 150 tiles of 4 096, more than
+    the launch's 8 workgroups per CU: the kernel walks the extra tiles
+    grid-stride.  A sample of 30 000 candidates from everywhere plus every
+    candidate of the first and the last address equal the oracle's
+    GetRSSCPUCore (rss.c:90-103); nothing written past the end."""
+    num_addr, nq = 200, 7
+    base_h, daddr_h, dport_h = 0x0A010001, 0xAC100002, 5201
+    total = num_addr * 64511
+    q = torch.full((total + 64,), 0xAA, dtype=torch.uint8, device=DEV)
+    cache = oracle.key_cache(oracle.KEY_0X05)
+    with gpu.Context() as ctx:
+        ctx.rss_queue_map_dev(base_h, num_addr, daddr_h, dport_h, nq, True, q)
+        ctx.sync()
+    got = q.cpu().numpy()
+    assert (got[total:] == 0xAA).all()
+    rng = np.random.default_rng(11)
+    idx = np.unique(np.concatenate([rng.integers(0, total, 30000), np.arange(64511),
+                                    np.arange(total - 64511, total)]))
+    for g in idx:
+        i, port = divmod(int(g), 64511)
+        want = oracle.rss_cpu_core(cache, daddr_h, base_h + i, dport_h, 1025 + port, nq, 1)
+        assert got[g] == want, (i, port)
