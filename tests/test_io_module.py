@@ -360,3 +360,17 @@ def test_two_threads_on_two_nodes_open_their_nodes_gpus(tmp_path, golden):
     drop = rx_drops(golden)
     assert stats["offloading_threads"] == 2
     assert np.array_equal(status == 0, drop) and (status[~drop] == 1).all()
+
+
+def test_staging_copies_are_exact(tmp_path):
+    """host_copy.hpp's streaming copies into the rxq staging (SSE2, and the
+    AVX-512 form the library picks at run time where the host has it) equal
+    memcpy for every length 0..2112 from every source alignment, and write
+    nothing past the slot's next 16 B."""
+    exe = tmp_path / "stage_copy_test"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "c", "stage_copy_test.cpp")], check=True)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0 and r["bad_sse"] == 0 and r["bad_avx512"] == 0, r
+    assert r["cases"] == 64 * 2113
