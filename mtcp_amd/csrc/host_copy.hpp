@@ -3,16 +3,14 @@
 #pragma once
 
 #include <emmintrin.h>
-#include <immintrin.h>
 #include <stdint.h>
 #include <string.h>
 
 // Copy a frame into its 64 B-aligned staging slot with streaming stores:
 // the slot is read next by the DMA engine, not by this core, so the stores
 // skip the read-for-ownership of a normal memcpy.  The slot's tail up to the
-// next 16 B is written too (it belongs to the slot's padding).  SSE2 form
-// (any x86-64 host):
-static inline void stage_copy_sse(uint8_t *dst, const uint8_t *src, uint32_t len) {
+// next 16 B is written too (it belongs to the slot's padding).
+static inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t len) {
     uint32_t i = 0;
     for (; i + 64 <= len; i += 64) {
         const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i));
@@ -32,34 +30,6 @@ static inline void stage_copy_sse(uint8_t *dst, const uint8_t *src, uint32_t len
         memcpy(t, src + i, len - i);
         _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), _mm_load_si128(reinterpret_cast<const __m128i *>(t)));
     }
-}
-
-// The same with 64 B streaming stores (a whole line each) where the host
-// has AVX-512 (Zen 4/5 EPYC, Xeon): a quarter of the store instructions.
-// dst is 64 B aligned (staging slots are).
-__attribute__((target("avx512f"))) static inline void stage_copy_avx512(uint8_t *dst, const uint8_t *src,
-                                                                        uint32_t len) {
-    uint32_t i = 0;
-    for (; i + 128 <= len; i += 128) {
-        const __m512i a = _mm512_loadu_si512(reinterpret_cast<const void *>(src + i));
-        const __m512i b = _mm512_loadu_si512(reinterpret_cast<const void *>(src + i + 64));
-        _mm512_stream_si512(reinterpret_cast<__m512i *>(dst + i), a);
-        _mm512_stream_si512(reinterpret_cast<__m512i *>(dst + i + 64), b);
-    }
-    for (; i + 64 <= len; i += 64)
-        _mm512_stream_si512(reinterpret_cast<__m512i *>(dst + i),
-                            _mm512_loadu_si512(reinterpret_cast<const void *>(src + i)));
-    if (i < len) stage_copy_sse(dst + i, src + i, len - i);   // the last < 64 B (16 B aligned)
-}
-
-static inline bool host_has_avx512() {
-    static const bool yes = __builtin_cpu_supports("avx512f");
-    return yes;
-}
-
-static inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t len) {
-    if (host_has_avx512()) stage_copy_avx512(dst, src, len);
-    else stage_copy_sse(dst, src, len);
 }
 
 // Make the streaming stores of stage_copy visible before a DMA reads them.

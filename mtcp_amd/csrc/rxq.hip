@@ -53,7 +53,6 @@ struct mtcp_gpu_rxq {
     // MTCP_GPU_SERVE_AHEAD=k prefetches frame i + k's header and result when
     // frame i is served (0: off)
     bool plain = false;
-    bool sse = false;                    // MTCP_GPU_STAGE=sse: the SSE2 streaming copy even with AVX-512
     uint32_t ahead = kServeAhead;
     uint32_t hint = 3;                   // MTCP_GPU_SERVE_HINT: prefetch locality 0..3
 };
@@ -106,10 +105,7 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     q->max_bytes = (max_bytes + 63) & ~63ull;
     q->stream = reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx));
     q->rec = mtcp_gpu_record_size(ctx);
-    if (const char *e = getenv("MTCP_GPU_STAGE")) {
-        q->plain = strcmp(e, "plain") == 0;
-        q->sse = strcmp(e, "sse") == 0;
-    }
+    if (const char *e = getenv("MTCP_GPU_STAGE")) q->plain = strcmp(e, "plain") == 0;
     if (const char *e = getenv("MTCP_GPU_SERVE_AHEAD")) q->ahead = (uint32_t)atoi(e);
     if (const char *e = getenv("MTCP_GPU_SERVE_HINT")) q->hint = (uint32_t)atoi(e);
     const uint64_t staging = q->max_bytes + (uint64_t)max_pkts * sizeof(mtcp_gpu_desc);
@@ -188,7 +184,6 @@ int mtcp_gpu_rxq_push(mtcp_gpu_rxq *q, const uint8_t *frame, uint16_t len) {
     d.flags = d.rsvd = 0;
     if (len) {
         if (q->plain) memcpy(q->buf + q->used, frame, len);
-        else if (q->sse) stage_copy_sse(q->buf + q->used, frame, len);
         else stage_copy(q->buf + q->used, frame, len);
     }
     q->used += slot;

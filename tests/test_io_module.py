@@ -363,10 +363,9 @@ def test_two_threads_on_two_nodes_open_their_nodes_gpus(tmp_path, golden):
 
 
 def test_staging_copies_are_exact(tmp_path):
-    """host_copy.hpp's streaming copies into the rxq staging (SSE2, and the
-    AVX-512 form the library picks at run time where the host has it) equal
-    memcpy for every length 0..2112 from every source alignment, and write
-    nothing past the slot's next 16 B."""
+    """host_copy.hpp's streaming copy into the rxq staging equals memcpy for
+    every length 0..2112 from every source alignment, and writes nothing past
+    the slot's next 16 B."""
     exe = tmp_path / "stage_copy_test"
     subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe),
                     os.path.join(ROOT, "tests", "c", "stage_copy_test.cpp")], check=True)

@@ -255,28 +255,6 @@ def main():
                     ref["pinned"] = "gpu_local_cpus"
                     print(json.dumps(ref), flush=True)
         return
-    if "--stage-ab" in sys.argv:
-        # the staging copy: AVX-512 64 B streaming stores (default where the
-        # host has them) against the SSE2 16 B form (MTCP_GPU_STAGE=sse);
-        # every thread offloads, 1 and 2 threads, interleaved
-        host = host_topology()
-        print(json.dumps(host), flush=True)
-        os.environ["RXLOOP_CPUS"] = ",".join(map(str, host["gpu_local_cpus"]))
-        os.environ["MTCP_GPU_THREADS"] = "all"
-        with tempfile.TemporaryDirectory() as tmp:
-            for rep in range(3):
-                for size, seed in ((1500, 2), (64, 1)):
-                    for threads in (1, 2):
-                        for stage in ("avx512", "sse"):
-                            os.environ.pop("MTCP_GPU_STAGE", None)
-                            if stage == "sse":
-                                os.environ["MTCP_GPU_STAGE"] = "sse"
-                            os.environ["RXLOOP_PASSES"] = "8"
-                            r = run(n, size, seed, tmp, "timing", threads, True, reps=1)
-                            print(json.dumps({"probe": "stage_ab", "rep": rep, "frame_size": size,
-                                              "threads": threads, "stage": stage,
-                                              "mpkt_per_s": r["mpkt_per_s"], "GBs": r["GBs"]}), flush=True)
-        return
     if "--threads-sweep" in sys.argv:
         # thread scaling at 1500 B, timing mode: threads pinned to CPUs of
         # the GPU's NUMA node, pinned to the first CPUs the process may use
