@@ -503,6 +503,75 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void l
         }
     }
 }
+// Probe (round 4): the same run walk with the run image filled by LDS-DMA
+// (global_load_lds_dwordx4: each wave-instruction lands 1 KiB straight in
+// LDS, no VGPR -> LDS write pass), then per-frame sums from LDS.  Timing
+// only, like lds_run_walk.
+template <int U>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void lds_dma_walk(mg::KParams kp) {
+    __shared__ v4u img[4][U * 64];
+    const uint32_t lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+    const uint32_t row = lane >> 4, rlane = lane & 15;
+    const uint32_t wave = blockIdx.x * 4 + wib, nw = gridDim.x * 4;
+    const uint64_t base = (uint64_t)(uintptr_t)kp.buf;
+    v4u *im = img[wib];
+    for (uint32_t g0 = 0; g0 < kp.n; g0 += nw * 64) {
+        const uint32_t k = g0 + (lane / 8) * (nw * 8) + wave * 8 + (lane % 8);
+        uint64_t lo = 0, hi = 0;
+        uint32_t nch = 0;
+        if (k < kp.n) {
+            const uint64_t raw = *reinterpret_cast<const uint64_t *>(kp.desc + k);
+            const uint64_t p = base + ((uint64_t)(uint32_t)raw << kp.off_shift);
+            const uint32_t L = (uint32_t)(raw >> 32) & 0xFFFFu;
+            lo = p & ~15ull;
+            hi = (p + L + 15) & ~15ull;
+            nch = L ? (uint32_t)((hi - lo) >> 4) : 0u;
+        }
+#pragma unroll 1
+        for (int j = 0; j < 8; ++j) {
+            const uint64_t rlo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(lo >> 32), 8 * j) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lo, 8 * j);
+            const uint64_t rhi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hi >> 32), 8 * j + 7) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hi, 8 * j + 7);
+            const uint32_t nc = rlo == 0 || rhi <= rlo ? 0u : (uint32_t)((rhi - rlo) >> 4);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = u * 64 + lane;
+                const uint32_t cc = c < nc ? c : (nc ? nc - 1 : 0u);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(rlo + 16ull * cc),
+                                                 (__attribute__((address_space(3))) void *)(im + u * 64),
+                                                 16, 0, 0);
+            }
+            __builtin_amdgcn_s_waitcnt(0);   // (coarse: every counter)
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int src = 8 * j + 4 * h + (int)row;
+                const uint32_t f_n = shfl32(nch, src);
+                const uint32_t f_lo = shfl32((uint32_t)lo, src);
+                const uint32_t s = (f_lo - (uint32_t)rlo) >> 4;
+                uint32_t acc = 0;
+                v4u y[6];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    const uint32_t c = u * 16 + rlane;
+                    y[u] = im[s + (c < f_n ? c : 0u)];
+                }
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    const uint32_t c = u * 16 + rlane;
+                    const uint32_t v = halves4(y[u], 0u);
+                    acc += c < f_n ? v : 0u;
+                }
+                acc = row_sum(acc);
+                const uint32_t kk = g0 + j * (nw * 8) + wave * 8 + 4 * h + row;
+                if (rlane == 15 && kk < kp.n) kp.out[kk].saddr = acc;
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
 }  // namespace mg
 
 struct Variant { const char *name; kfn fn; uint32_t blocks_per_cu; uint32_t wpb = 4; };
@@ -709,6 +778,7 @@ int main(int argc, char **argv) {
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
         vs.push_back({"b16_rss_sorted6_cmp_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, true>, 2});
         vs.push_back({"ldsrun12_cu2", lds_run_walk<12>, 2});
+        vs.push_back({"ldsdma12_cu2", lds_dma_walk<12>, 2});
         vs.push_back({"rss_sorted6_wpb8_cu1", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 8>, 1, 8});
         vs.push_back({"rss_sorted6_wpb2_cu4", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 0, 2>, 4, 2});
         vs.push_back({"rss_sorted6_prio1half_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 8, true, 6, false, false, 5>, 2});
@@ -841,6 +911,7 @@ int main(int argc, char **argv) {
         vs.push_back({"runstream8_cu2", run_stream<8>, 2});
         vs.push_back({"runstream12_cu2", run_stream<12>, 2});
         vs.push_back({"ldsrun12_cu2", lds_run_walk<12>, 2});
+        vs.push_back({"ldsdma12_cu2", lds_dma_walk<12>, 2});
         // tx fill last: it repairs the corrupted frames the rx variants compare on
         vs.push_back({"tx_unrolled_cu2", rx_kernel<kTxChunk, false, 3>, 2});
         vs.push_back({"tx_unrolled_nodefer_cu2", rx_kernel<kTxChunk, false, 3, false, 0, 0>, 2});
@@ -902,7 +973,7 @@ int main(int argc, char **argv) {
                     return 2;
                 }
             }
-            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "wpp") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && !strstr(vs[v].name, "runstream") && !strstr(vs[v].name, "ldsrun") && !strstr(vs[v].name, "_cmp")) {
+            if (v > 0 && r == 0 && !strstr(vs[v].name, "abl") && !strstr(vs[v].name, "wpp") && !strstr(vs[v].name, "norss") && strncmp(vs[v].name, "tx_", 3) != 0 && !strstr(vs[v].name, "plain") && !strstr(vs[v].name, "lad") && !strstr(vs[v].name, "runstream") && !strstr(vs[v].name, "ldsrun") && !strstr(vs[v].name, "ldsdma") && !strstr(vs[v].name, "_cmp")) {
                 std::vector<mtcp_gpu_result> x(n), y(n);
                 CK(hipMemcpy(x.data(), d_ref, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
                 CK(hipMemcpy(y.data(), d_out, n * sizeof(mtcp_gpu_result), hipMemcpyDeviceToHost));
