@@ -7,7 +7,7 @@ ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
 LIB      := mtcp_amd/lib/libmtcp_gpu.so
 SRCS     := mtcp_amd/csrc/mtcp_gpu.hip mtcp_amd/csrc/pktgen.hip mtcp_amd/csrc/rxq.hip
-DEPS     := $(SRCS) mtcp_amd/csrc/rx_kernels.hpp mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/host_copy.hpp mtcp_amd/csrc/flow_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h include/mtcp_gpu_rxq.h
+DEPS     := $(SRCS) mtcp_amd/csrc/rx_kernels.hpp mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/rx_span.hpp mtcp_amd/csrc/host_copy.hpp mtcp_amd/csrc/flow_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h include/mtcp_gpu_rxq.h
 
 .PHONY: all lib oracle ref golden examples clean tools
 
@@ -69,7 +69,7 @@ tests/c/admit_test: tests/c/admit_test.c mtcp_amd/io_module/gpu_module.c $(LIB)
 	gcc -std=gnu99 -O1 -Wall -pthread -Itests/c/mtcp_double -Iinclude -o $@ tests/c/admit_test.c \
 	    oracle/mtcp_oracle.c -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib'
 
-tools/wave_probe: tools/wave_probe.hip mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/rx_kernels.hpp $(LIB)
+tools/wave_probe: tools/wave_probe.hip mtcp_amd/csrc/rx_span.hpp mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/rx_kernels.hpp $(LIB)
 	$(HIPCC) $(TOOLFLAGS) -o $@ $< -Lmtcp_amd/lib -lmtcp_gpu -Wl,-rpath,'$$ORIGIN/../mtcp_amd/lib'
 
 tools/occ_probe: tools/occ_probe.hip mtcp_amd/csrc/rx_kernels.hpp $(LIB)

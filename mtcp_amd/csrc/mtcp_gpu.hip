@@ -18,7 +18,7 @@
 #include "flow_kernels.hpp"
 #include "host_copy.hpp"
 #include "rx_kernels.hpp"
-#include "rx_wave.hpp"
+#include "rx_span.hpp"
 
 namespace {
 
@@ -216,19 +216,31 @@ constexpr uint32_t kHeldPasses = 8;
 // quad) on every packet.  The choice by batch size and average slot, from
 // tools/wave_probe.hip and tools/small_batch_probe.py (same frames, same
 // process):
-//   slot < 256 B:   n <= 2 048  wave;  n <= 128 K a quad per packet (256 per workgroup)
+//   slot < 256 B:   n <= 2 048  wave;  n <= 128 K a quad per packet (64 per workgroup)
 //   slot > 4 KiB:   n <= 64 K   wave (a jumbo frame in one trip)
 //   otherwise:      n <= 8 192  wave;  n <= 32 K  a row per packet (64 per workgroup)
-//   larger batches: rx_kernel (64 packets per wave)
+//   larger batches: slot <= 64 B a quad per packet; slot <= 640 B rx_span_kernel
+//                   (rx_span.hpp: the workgroup's chunks back to back, whatever
+//                   the sizes); above, rx_kernel (64 packets per wave)
 // (since the select-form per-lane phase 2: 4 096 x 64 B quad 3.55 vs wave
 // 3.86 us, 2 048 x 64 B 3.53 vs 3.21; 8 192 x 1500 B wave 6.05 vs row 7.32,
 // 16 K 9.31 vs 7.35: profiles/r2/wave_probe_dispatch.jsonl; 128 K x 64 B quad 5.37
-// vs rx_kernel 6.05 us through the Python ABI: profiles/r2/small_batch_sched.jsonl)
+// vs rx_kernel 6.05 us through the Python ABI: profiles/r2/small_batch_sched.jsonl.
+// Round 4, profiles/r4/group_span_probe.jsonl: quads in 256-thread workgroups
+// beat the 1024-thread ones at every n (1 M x 64 B 24.9 vs 31.5 us, rx_kernel
+// 32.3); on 1 M frames of 128 / 256 / 512 B rx_span_kernel takes 39.7 / 60.3 /
+// 101.9 us where rx_kernel's rows take 122.6 / 126.5 / 136.1, and on an IMIX
+// (64 / 576 / 1500 B, 7 : 4 : 1) 77.8 vs 86.1 us; from 768 B slots on
+// rx_kernel is ahead again, 142.4 vs 146.4 us.)
 // Pointer bursts carry no size the host can see: they count as mid-size.
-// MTCP_GPU_SCHED=wave|row|quad|big at context open forces one kernel for
+// MTCP_GPU_SCHED=wave|row|quad|span|big at context open forces one kernel for
 // every batch (A/B runs, and the parity tests of each); the tx fill of
-// pointer bursts and the tx report exist only in the small kernels.
-enum Sched : int { kSchedAuto = 0, kSchedWave, kSchedRow, kSchedQuad, kSchedBig };
+// pointer bursts and the tx report exist only in the small kernels, and the
+// span kernel is rx only (a forced span runs tx on rx_kernel).
+enum Sched : int { kSchedAuto = 0, kSchedWave, kSchedRow, kSchedQuad, kSchedBig, kSchedSpan };
+
+constexpr uint64_t kQuadOnlyUpToSlot = 64;
+constexpr uint64_t kSpanUpToSlot = 640;
 
 int sched_from_env() {
     const char *e = getenv("MTCP_GPU_SCHED");
@@ -236,17 +248,21 @@ int sched_from_env() {
     if (!strcmp(e, "wave")) return kSchedWave;
     if (!strcmp(e, "row")) return kSchedRow;
     if (!strcmp(e, "quad")) return kSchedQuad;
+    if (!strcmp(e, "span")) return kSchedSpan;
     if (!strcmp(e, "big")) return kSchedBig;
     return kSchedAuto;
 }
 
-int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_only) {
+// rx: the batch is an rx launch (the span kernel exists for rx only)
+int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_only, bool rx) {
     int s = ctx->sched;
     if (s == kSchedAuto) {
-        if (slot < 256) s = n <= 2048 ? kSchedWave : n <= (1u << 17) ? kSchedQuad : kSchedBig;
+        const int big = slot <= kQuadOnlyUpToSlot ? kSchedQuad : slot <= kSpanUpToSlot ? kSchedSpan : kSchedBig;
+        if (slot < 256) s = n <= 2048 ? kSchedWave : n <= (1u << 17) ? kSchedQuad : big;
         else if (slot > 4096) s = n <= (1u << 16) ? kSchedWave : kSchedBig;
-        else s = n <= 8192 ? kSchedWave : n <= (1u << 15) ? kSchedRow : kSchedBig;
+        else s = n <= 8192 ? kSchedWave : n <= (1u << 15) ? kSchedRow : big;
     }
+    if (s == kSchedSpan && !rx) s = kSchedBig;
     if (s == kSchedBig && small_only) s = kSchedRow;
     return s;
 }
@@ -269,10 +285,17 @@ const char *launch_small(int sched, uint32_t n, uint64_t slot, hipStream_t st, c
         hipLaunchKernelGGL((mg::rx_wave_kernel<MODE, RSS>), grid, dim3(mg::kBlock), 0, st, kp);
         return "rx_wave_kernel<10 loads>";
     } else if (sched == kSchedQuad) {
-        constexpr uint32_t P = mg::GroupShape<4>::P;
-        hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 4>), dim3((n + P - 1) / P), dim3(mg::kGroupBlock), 0,
+        constexpr int kBlk = mg::kQuadBlock;
+        constexpr uint32_t P = mg::GroupShape<4, kBlk>::P;
+        hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 4, 0, 1, kBlk>), dim3((n + P - 1) / P), dim3(kBlk), 0,
                            st, kp);
         return "rx_group_kernel<quad>";
+    } else if (sched == kSchedSpan) {
+        if constexpr (!mg::is_tx(MODE)) {
+            hipLaunchKernelGGL((mg::rx_span_kernel<MODE, RSS>), dim3((n + mg::kSpanP - 1) / mg::kSpanP),
+                               dim3(mg::kSpanBlock), 0, st, kp);
+            return "rx_span_kernel";
+        }
     }
     constexpr uint32_t P = mg::GroupShape<16>::P;
     hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 16>), dim3((n + P - 1) / P), dim3(mg::kGroupBlock), 0,
@@ -290,7 +313,8 @@ int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
     const bool rss = !mg::is_tx(MODE) && (ctx->flags & MTCP_GPU_F_RSS);
     const bool ptrs = MODE == mg::kRxPtrs || MODE == mg::kTxPtrs;
     const uint64_t avg_slot = ptrs ? 1024 : kp.buf_len / kp.n;
-    const int sched = pick_sched(ctx, kp.n, avg_slot, MODE == mg::kTxPtrs || kp.tx_report != nullptr);
+    const int sched = pick_sched(ctx, kp.n, avg_slot, MODE == mg::kTxPtrs || kp.tx_report != nullptr,
+                                 !mg::is_tx(MODE));
     if (sched != kSchedBig) {
         ctx->last_kernel = rss ? launch_small<MODE, true>(sched, kp.n, avg_slot, st, kp)
                                : launch_small<MODE, false>(sched, kp.n, avg_slot, st, kp);

@@ -327,12 +327,21 @@ __global__ __launch_bounds__(kWave * WPB) void rx_wave_kernel(KParams kp) {
 // instruction stream (parse_finish, the code rx_kernel runs), so phase 2
 // costs 1/P of the wave-uniform version's issue slots.
 constexpr int kGroupBlock = 1024;              // 16 waves
+// Quads run in 256-thread workgroups (P = 64: one full phase-2 wave, and
+// four times the workgroups in flight): 1 M x 64 B 24.9 vs 31.5 us in
+// 1024-thread ones, 4 096 x 64 B 2.76 vs 3.23 (tools/wave_probe g4b256 / g4,
+// profiles/r4/group_span_probe.jsonl).  Rows keep 1024: at 2-4 K MTU frames
+// the 256-thread rows lose (5.9 vs 4.2 us).
+constexpr int kQuadBlock = 256;
 
-template <int G>
+// BLK: threads per workgroup (P = BLK / G packets).  U: 16 B loads per lane
+// per trip (0: by G).
+template <int G, int BLK = kGroupBlock, int U_ = 0>
 struct GroupShape {
-    static_assert(G == 4 || G == 16 || G == 64, "lanes per packet: a quad, a row or the wave");
-    static constexpr int P = kGroupBlock / G;                   // packets per workgroup
-    static constexpr int U = G == 64 ? 8 : G == 16 ? 6 : 2;     // loads per lane per trip
+    static_assert(G == 4 || G == 8 || G == 16 || G == 64, "lanes per packet: a quad, 8 lanes, a row or the wave");
+    static_assert(BLK % kWave == 0 && BLK >= G && BLK <= 1024, "whole waves, at most 1024 threads");
+    static constexpr int P = BLK / G;                           // packets per workgroup
+    static constexpr int U = U_ ? U_ : G == 64 ? 8 : G == 16 ? 6 : G == 8 ? 4 : 2;   // loads per lane per trip
     static constexpr int R = G >= 16 ? G / 16 : 1;              // partial sums per packet
     static constexpr int S = P + 1;                             // LDS stride (odd: no conflicts)
     static constexpr int W2 = (P + kWave - 1) / kWave;          // waves that run phase 2
@@ -341,19 +350,19 @@ struct GroupShape {
 // ABL (profiling only, tools/wave_probe.hip): 1 = phase 2 stores the sum only.
 // AL: phase 2 takes parse_finish's ALIGNED form when every frame of the wave
 // starts on a 4-byte boundary (AL 0: never; an A/B baseline).
-template <int MODE, bool RSS, int G, int ABL = 0, int AL = 1>
-__global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
+template <int MODE, bool RSS, int G, int ABL = 0, int AL = 1, int BLK = kGroupBlock, int U_ = 0>
+__global__ __launch_bounds__(BLK) void rx_group_kernel(KParams kp) {
 #ifndef MTCP_GPU_TESTING
     static_assert(ABL == 0, "the ABL (profiling) variants need a -DMTCP_GPU_TESTING build (tools/)");
 #endif
-    using Sh = GroupShape<G>;
+    using Sh = GroupShape<G, BLK, U_>;
     constexpr int P = Sh::P, U = Sh::U, R = Sh::R, S = Sh::S;
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
     __shared__ uint32_t hd[kHdRows * S];       // dword i of packet q at hd[i * S + q]
     __shared__ uint32_t psum[P * R];
     __shared__ uint4 info[P];                  // {p lo, p hi, L | ok << 16, nch}
     if constexpr (RSS) {
-        for (int i = threadIdx.x; i < kRssTableWords; i += kGroupBlock) rss_lds[i] = kp.rss_tables[i];
+        for (int i = threadIdx.x; i < kRssTableWords; i += BLK) rss_lds[i] = kp.rss_tables[i];
     }
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wib = threadIdx.x >> 6;
@@ -414,9 +423,11 @@ __global__ __launch_bounds__(kGroupBlock) void rx_group_kernel(KParams kp) {
             }
         }
     }
-    if constexpr (G == 4) {
+    if constexpr (G <= 8) {
         acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
         acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+        if constexpr (G == 8)
+            acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x141, 0xF, 0xF, false);  // row_half_mirror
         if (gl == 0) psum[pkt] = acc;
     } else {
         acc = row_sum(acc);

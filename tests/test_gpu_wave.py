@@ -2,8 +2,8 @@
 (mtcp_amd/csrc/rx_wave.hpp), on the MI355X, bit-exact:
 
 * every dispatched kernel — a wavefront, a 16-lane row or a 4-lane quad per
-  packet (rx_wave.hpp) and rx_kernel's sorted / unrolled / line-aligned
-  rounds, each forced with MTCP_GPU_SCHED (mtcp_gpu.hip pick_sched) — on the
+  packet (rx_wave.hpp), the chunk-parallel span kernel (rx_span.hpp) and
+  rx_kernel's sorted / unrolled / line-aligned rounds, each forced with MTCP_GPU_SCHED (mtcp_gpu.hip pick_sched) — on the
   golden vectors and on config-shaped batches of 4 096 (one io_module
   aggregate) and 65 536 packets, against the reference's results and the
   oracle;
@@ -41,7 +41,8 @@ def gpu():
 
 def ctx_for(gpu, monkeypatch, sched, **kw):
     """A context whose batches all take kernel `sched` (mtcp_gpu.hip
-    MTCP_GPU_SCHED): "wave", "row", "quad" (rx_wave.hpp) or "big" (rx_kernel)."""
+    MTCP_GPU_SCHED): "wave", "row", "quad" (rx_wave.hpp), "span" (rx_span.hpp)
+    or "big" (rx_kernel)."""
     monkeypatch.setenv("MTCP_GPU_SCHED", sched)
     c = gpu.Context(0, **kw)
     monkeypatch.delenv("MTCP_GPU_SCHED")
@@ -54,7 +55,7 @@ def ptr_burst(b, desc):
     return ptrs, lens
 
 
-SCHEDS = ["wave", "row", "quad", "big"]
+SCHEDS = ["wave", "row", "quad", "span", "big"]
 
 
 @pytest.mark.parametrize("sched", SCHEDS)
@@ -103,19 +104,76 @@ def test_small_batches_every_schedule(gpu, monkeypatch, n, size, rss):
     assert (want["verdict"] == 0).mean() > 0.99
 
 
-@pytest.mark.parametrize("n,size", [(2048, 64), (2049, 64), (1 << 17, 64), (8192, 1500), (8193, 1500)])
-def test_dispatch_boundaries(gpu, monkeypatch, n, size):
+def imix_lengths(n, seed):
+    """64 / 576 / 1500 B frames in the ratio 7 : 4 : 1 (simple IMIX)."""
+    r = np.random.default_rng(seed).integers(0, 12, n)
+    return np.where(r < 7, 64, np.where(r < 11, 576, 1500)).astype(np.uint16)
+
+
+@pytest.mark.parametrize("n,size,kernel", [
+    (2048, 64, "rx_wave"), (2049, 64, "rx_group_kernel<quad"), (1 << 17, 64, "rx_group_kernel<quad"),
+    ((1 << 17) + 1, 64, "rx_group_kernel<quad"), ((1 << 17) + 1, 128, "rx_span_kernel"),
+    (8192, 1500, "rx_wave"), (8193, 1500, "rx_group_kernel<row"), (32768, 512, "rx_group_kernel<row"),
+    (32769, 512, "rx_span_kernel"), (32769, 640, "rx_span_kernel"), (32769, 704, "rx_kernel"),
+    ((1 << 18) + 3, "imix", "rx_span_kernel")])
+def test_dispatch_boundaries(gpu, monkeypatch, n, size, kernel):
     """The automatic kernel choice (mtcp_gpu.hip pick_sched) on both sides of
     each boundary it draws — small frames: wave up to 2 048, quad up to
-    128 K; MTU frames: wave up to 8 192, row above — equal to the oracle."""
+    128 K, then quads for 64 B slots and the span kernel for larger ones; MTU
+    frames: wave up to 8 192, row above; past 32 K frames of <= 640 B slots
+    the span kernel — each the kernel it should be, and equal to the oracle."""
     monkeypatch.delenv("MTCP_GPU_SCHED", raising=False)
     seed = 67
-    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    if size == "imix":
+        desc, nbytes = pktgen.layout_from_lengths(imix_lengths(n, seed), 6)
+    else:
+        desc, nbytes = pktgen.layout(n, size, 6, seed)
     buf = np.zeros(nbytes, np.uint8)
     oracle.pktgen(buf, desc, 6, seed, 0)
     want = oracle.rx_chunk(buf, desc, 6)
     with gpu.Context(0) as ctx:
         assert_same(run_rx_dev(ctx, buf, desc, 6), want, f"auto {size} x {n}")
+        assert ctx.last_kernel.startswith(kernel), ctx.last_kernel
+
+
+@pytest.mark.parametrize("sizes", ["imix", "ragged"])
+def test_span_kernel_mixed_sizes(gpu, monkeypatch, sizes):
+    """rx_span_kernel on the batches it exists for — an IMIX, and frames of
+    every length 1 .. 2 000 B with empty descriptors, out-of-buffer ones and
+    runs of one-chunk frames between them — chunk and pointer modes, with RSS
+    and the fused flow bins, equal to the oracle."""
+    rng = np.random.default_rng(73)
+    n = 20000 + 37
+    if sizes == "imix":
+        lens = imix_lengths(n, 73)
+    else:
+        lens = rng.integers(1, 2001, n).astype(np.uint16)
+        lens[rng.random(n) < .1] = 0
+        lens[rng.random(n) < .1] = 14
+    desc, nbytes = pktgen.layout_from_lengths(lens, 6)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, 73, 0)
+    if sizes == "ragged":
+        bad = rng.random(n) < .01
+        desc["offset"][bad] = (nbytes >> 6) + 5                     # past the buffer
+    want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(None, 8, 1))
+    with ctx_for(gpu, monkeypatch, "span", rss=True, rss_queues=8, rss_endian=True) as ctx:
+        got = run_rx_dev(ctx, buf, desc, 6)
+        assert ctx.last_kernel == "rx_span_kernel"
+        b = to_dev(buf)
+        bdesc = desc.copy()
+        bdesc["offset"] = desc["offset"].astype(np.int64) << 6
+        ok = desc["offset"].astype(np.int64) << 6 < nbytes
+        bdesc["offset"][~ok] = 0
+        ptrs, lns = ptr_burst(b, bdesc)
+        out = dev_results(n)
+        bins = torch.zeros(n, dtype=torch.int32, device=DEV)
+        ctx.rx_ptrs_flow_dev(ptrs, lns, n, out, bins)
+        torch.cuda.synchronize()
+    assert_same(got, want, f"span {sizes} chunk")
+    gp = out.cpu().numpy().view(RESULT_DTYPE)
+    assert_same(gp[ok], want[ok], f"span {sizes} pointers")
+    assert np.array_equal(bins.cpu().numpy().view(np.uint32)[ok], oracle.flow_bins(want)[ok])
 
 
 def test_short_trip_kernel_with_jumbo_frames(gpu, monkeypatch):

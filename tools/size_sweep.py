@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Frame-size sweep of the rx path (a measurement tool, not product code):
+for each fixed frame size, a batch of ~1.5 GB of synthetic frames resident
+in HBM, 50 back-to-back mtcp_gpu_rx_chunk_dev launches timed with HIP events
+on the launch stream, next to the box's read ceiling on the same buffer
+(tools/libstream_ceiling.so).  One JSON line per size: the kernel the
+dispatcher picked, its time, Σ L / t against 8 TB/s and against the stream.
+  usage: python tools/size_sweep.py [sizes...]"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from mtcp_amd import gpu, pktgen  # noqa: E402
+
+SIZES = [64, 128, 256, 384, 512, 768, 1024, 1500, 2048, 4096, 9000]
+
+
+def ceiling_us(buf, nbytes, stream):
+    f = ctypes.CDLL(os.path.join(ROOT, "tools", "libstream_ceiling.so")).stream_ceiling_us
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
+                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    us, shape = ctypes.c_float(0.0), ctypes.c_int(0)
+    if f(buf.data_ptr(), nbytes, 20, stream.cuda_stream, ctypes.byref(us), ctypes.byref(shape)) != 0:
+        raise RuntimeError("stream_ceiling_us failed")
+    return float(us.value)
+
+
+def main():
+    sizes = [int(a) for a in sys.argv[1:]] or SIZES
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    for size in sizes:
+        slot = (size + 63) & ~63
+        n = min((3 << 29) // slot, 1 << 23)            # ~1.5 GB of slots, at most 8 M frames
+        desc, nbytes = pktgen.layout(n, size, 6, 7)
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        d = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+        out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+        gpu.pktgen_dev(buf, d, n, 6, 7, stream=stream)
+        with gpu.Context(0) as ctx:
+            ceil = ceiling_us(buf, nbytes, stream)
+            for _ in range(5):
+                ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 50
+            e0.record(stream)
+            for _ in range(reps):
+                ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            kernel = ctx.last_kernel
+        fb = int(desc["len"].astype(np.int64).sum())
+        print(json.dumps({"probe": "size_sweep", "frame_size": size, "frames": n, "kernel": kernel,
+                          "us_per_launch": round(us, 2), "GBs": round(fb / us / 1e3, 1),
+                          "gpkt_per_s": round(n / us / 1e3, 3), "frac_of_8TBs": round(fb / us / 8e6, 4),
+                          "ceiling_us": round(ceil, 2), "frac_of_ceiling": round(ceil / us, 4),
+                          "records_MB": round(n * 40 / 1e6, 1)}), flush=True)
+        del buf, d, out
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -6,7 +6,8 @@
 //   phase1     ABL 1: + the frame stream and the chunk sum
 //   full       the dispatched kernel (phase 2 and the record)
 //   rows       rx_kernel (the schedule mtcp_gpu.hip picks for big batches)
-// usage: tools/wave_probe [size] [n...]      size: 64 | 1500 | 9000
+// usage: tools/wave_probe [size] [n...]      size: bytes (64 .. 9000) | imix
+//   imix: 64 / 576 / 1500 B frames in the ratio 7 : 4 : 1, in a hashed order
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -17,7 +18,7 @@
 
 #include "../include/mtcp_gpu.h"
 #include "../include/mtcp_gpu_pktgen.h"
-#include "../mtcp_amd/csrc/rx_wave.hpp"
+#include "../mtcp_amd/csrc/rx_span.hpp"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -30,7 +31,14 @@ __global__ __launch_bounds__(64 * WPB) void empty_kernel(mg::KParams kp) {
 typedef void (*kfn)(mg::KParams);
 
 int main(int argc, char **argv) {
-    const uint32_t L = argc > 1 ? (uint32_t)atoi(argv[1]) : 1500;
+    const bool imix = argc > 1 && !strcmp(argv[1], "imix");
+    const uint32_t L = imix ? 0u : argc > 1 ? (uint32_t)atoi(argv[1]) : 1500;
+    auto len_of = [&](uint32_t i) -> uint32_t {
+        if (!imix) return L;
+        const uint32_t h = (i * 2654435761u) >> 16;
+        const uint32_t r = h % 12;
+        return r < 7 ? 64u : r < 11 ? 576u : 1500u;
+    };
     std::vector<uint32_t> ns;
     for (int i = 2; i < argc; ++i) ns.push_back((uint32_t)atoi(argv[i]));
     if (ns.empty()) ns = {64, 1024, 4096, 16384};
@@ -62,6 +70,25 @@ int main(int argc, char **argv) {
         {"g4", mg::rx_group_kernel<mg::kRxChunk, false, 4>, 1024, 256},
         {"g4noal", mg::rx_group_kernel<mg::kRxChunk, false, 4, 0, 0>, 1024, 256},
         {"g16noal", mg::rx_group_kernel<mg::kRxChunk, false, 16, 0, 0>, 1024, 64},
+        // workgroup size (P = 64 packets: one full phase-2 wave) and 8-lane groups
+        {"g4b256", mg::rx_group_kernel<mg::kRxChunk, false, 4, 0, 1, 256>, 256, 64},
+        {"g4b512", mg::rx_group_kernel<mg::kRxChunk, false, 4, 0, 1, 512>, 512, 128},
+        {"g8b256", mg::rx_group_kernel<mg::kRxChunk, false, 8, 0, 1, 256>, 256, 32},
+        {"g8b512", mg::rx_group_kernel<mg::kRxChunk, false, 8, 0, 1, 512>, 512, 64},
+        {"g8", mg::rx_group_kernel<mg::kRxChunk, false, 8>, 1024, 128},
+        {"g8u2b512", mg::rx_group_kernel<mg::kRxChunk, false, 8, 0, 1, 512, 2>, 512, 64},
+        {"g16b256", mg::rx_group_kernel<mg::kRxChunk, false, 16, 0, 1, 256>, 256, 16},
+        {"g16b512", mg::rx_group_kernel<mg::kRxChunk, false, 16, 0, 1, 512>, 512, 32},
+        {"g16u2", mg::rx_group_kernel<mg::kRxChunk, false, 16, 0, 1, 1024, 2>, 1024, 64},
+        {"g4b128", mg::rx_group_kernel<mg::kRxChunk, false, 4, 0, 1, 128>, 128, 32},
+        {"g4b64", mg::rx_group_kernel<mg::kRxChunk, false, 4, 0, 1, 64>, 64, 16},
+        {"g8b128", mg::rx_group_kernel<mg::kRxChunk, false, 8, 0, 1, 128>, 128, 16},
+        {"g8u2b256", mg::rx_group_kernel<mg::kRxChunk, false, 8, 0, 1, 256, 2>, 256, 32},
+        {"g8u6b256", mg::rx_group_kernel<mg::kRxChunk, false, 8, 0, 1, 256, 6>, 256, 32},
+        {"g16b128", mg::rx_group_kernel<mg::kRxChunk, false, 16, 0, 1, 128>, 128, 8},
+        {"span2", mg::rx_span_kernel<mg::kRxChunk, false, 2>, 256, 64},
+        {"span4", mg::rx_span_kernel<mg::kRxChunk, false, 4>, 256, 64},
+        {"span8", mg::rx_span_kernel<mg::kRxChunk, false, 8>, 256, 64},
         {"rows", mg::rx_kernel<mg::kRxChunk, false, mg::kSchedSorted>, 256, 0},
     };
     for (uint32_t n : ns) {
@@ -69,9 +96,9 @@ int main(int argc, char **argv) {
         uint64_t off = 0;
         for (uint32_t i = 0; i < n; ++i) {
             desc[i].offset = (uint32_t)(off >> 6);
-            desc[i].len = (uint16_t)L;
+            desc[i].len = (uint16_t)len_of(i);
             desc[i].flags = desc[i].rsvd = 0;
-            off += (L + 63) & ~63u;
+            off += (len_of(i) + 63) & ~63u;
         }
         uint8_t *d_buf;
         mtcp_gpu_desc *d_desc;
