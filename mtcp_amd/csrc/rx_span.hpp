@@ -65,9 +65,14 @@ __device__ __forceinline__ uint32_t span_find(uint32_t start, uint32_t j, uint32
 }
 
 // U: windows (64-chunk loads) in flight per wave.
-template <int MODE, bool RSS, int U = 4>
+// ABL (profiling only, tools/wave_probe.hip): 1 = phase 2 stores the sum
+// only; 2 = descriptors and the scan only (stores the chunk count).
+template <int MODE, bool RSS, int U = 4, int ABL = 0>
 __global__ __launch_bounds__(kSpanBlock) void rx_span_kernel(KParams kp) {
     static_assert(MODE == kRxChunk || MODE == kRxPtrs, "rx modes only");
+#ifndef MTCP_GPU_TESTING
+    static_assert(ABL == 0, "the ABL (profiling) variants need a -DMTCP_GPU_TESTING build (tools/)");
+#endif
     constexpr int P = kSpanP, S = P + 1;
     constexpr uint32_t kStride = kSpanWaves * kWave;          // chunks between a wave's windows
     __shared__ uint32_t rss_lds[RSS ? kRssTableWords : 1];
@@ -112,6 +117,10 @@ __global__ __launch_bounds__(kSpanBlock) void rx_span_kernel(KParams kp) {
     ps[lane] = 0;
     if (wib == 0) info[lane] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), L | ((uint32_t)ok << 16), nch);
     __builtin_amdgcn_wave_barrier();
+    if constexpr (ABL == 2) {
+        if (wib == 0 && k < kp.n) kp.out[k].saddr = nch;
+        return;
+    }
 
     // ---- the chunk stream ----------------------------------------------------------
     for (uint32_t base = wib * kWave; base < C; base += kStride * U) {      // wave-uniform
@@ -168,6 +177,10 @@ __global__ __launch_bounds__(kSpanBlock) void rx_span_kernel(KParams kp) {
     uint32_t sum = 0;
 #pragma unroll
     for (int w = 0; w < kSpanWaves; ++w) sum += psum[w][q];
+    if constexpr (ABL == 1) {
+        kp.out[k].saddr = sum;
+        return;
+    }
     Pkt pk;
     if (__ballot((pq & 3) != 0) == 0)
         pk = parse_finish<MODE, S, true, true>(hd + q, sum, pq, inf.z & 0xFFFFu, inf.w, (inf.z >> 16) & 1u);

@@ -6,8 +6,9 @@
 //   phase1     ABL 1: + the frame stream and the chunk sum
 //   full       the dispatched kernel (phase 2 and the record)
 //   rows       rx_kernel (the schedule mtcp_gpu.hip picks for big batches)
-// usage: tools/wave_probe [size] [n...]      size: bytes (64 .. 9000) | imix
+// usage: tools/wave_probe [size] [n...]      size: bytes (64 .. 9000) | imix | bimodal
 //   imix: 64 / 576 / 1500 B frames in the ratio 7 : 4 : 1, in a hashed order
+//   bimodal: 64 / 1500 B, p = 0.5 each (C3's mix, hashed order)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -32,10 +33,12 @@ typedef void (*kfn)(mg::KParams);
 
 int main(int argc, char **argv) {
     const bool imix = argc > 1 && !strcmp(argv[1], "imix");
-    const uint32_t L = imix ? 0u : argc > 1 ? (uint32_t)atoi(argv[1]) : 1500;
+    const bool bimodal = argc > 1 && !strcmp(argv[1], "bimodal");
+    const uint32_t L = imix || bimodal ? 0u : argc > 1 ? (uint32_t)atoi(argv[1]) : 1500;
     auto len_of = [&](uint32_t i) -> uint32_t {
-        if (!imix) return L;
         const uint32_t h = (i * 2654435761u) >> 16;
+        if (bimodal) return (h ^ (h >> 7)) & 1 ? 1500u : 64u;
+        if (!imix) return L;
         const uint32_t r = h % 12;
         return r < 7 ? 64u : r < 11 ? 576u : 1500u;
     };
@@ -48,7 +51,11 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     // threads per block and packets per block of each variant
-    struct V { const char *name; kfn fn; uint32_t threads, ppb; };
+    // ppb: packets per workgroup (0: a persistent grid, `persist` workgroups
+    // per CU, at most one 64-frame tile per wave; rx_kernel's grid when 0)
+    struct V { const char *name; kfn fn; uint32_t threads, ppb, persist = 0; };
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const V vs[] = {
         {"empty", empty_kernel<4>, 256, 4},
         {"empty16", empty_kernel<16>, 1024, 16},
@@ -89,6 +96,8 @@ int main(int argc, char **argv) {
         {"span2", mg::rx_span_kernel<mg::kRxChunk, false, 2>, 256, 64},
         {"span4", mg::rx_span_kernel<mg::kRxChunk, false, 4>, 256, 64},
         {"span8", mg::rx_span_kernel<mg::kRxChunk, false, 8>, 256, 64},
+        {"span4_p1", mg::rx_span_kernel<mg::kRxChunk, false, 4, 1>, 256, 64},
+        {"span4_desc", mg::rx_span_kernel<mg::kRxChunk, false, 4, 2>, 256, 64},
         {"rows", mg::rx_kernel<mg::kRxChunk, false, mg::kSchedSorted>, 256, 0},
     };
     for (uint32_t n : ns) {
@@ -127,7 +136,9 @@ int main(int argc, char **argv) {
         const bool sync_each = getenv("WP_SYNC") && atoi(getenv("WP_SYNC"));
         for (const V &v : vs) {
             if (only && !strstr(only, v.name)) continue;
-            const uint32_t blocks = v.ppb ? (n + v.ppb - 1) / v.ppb : std::min<uint32_t>((n + 255) / 256, 512);
+            const uint32_t blocks = v.ppb ? (n + v.ppb - 1) / v.ppb
+                                    : v.persist ? std::min<uint32_t>((n + 255) / 256, (uint32_t)cus * v.persist)
+                                                : std::min<uint32_t>((n + 255) / 256, 512);
             std::vector<float> t;
             for (int r = 0; r < rounds; ++r) {
                 for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(v.fn, dim3(blocks), dim3(v.threads), 0, st, kp);
