@@ -221,7 +221,8 @@ constexpr uint32_t kHeldPasses = 8;
 //   otherwise:      n <= 8 192  wave;  n <= 32 K  a row per packet (64 per workgroup)
 //   larger batches: slot <= 64 B a quad per packet; slot <= 640 B rx_span_kernel
 //                   (rx_span.hpp: the workgroup's chunks back to back, whatever
-//                   the sizes); above, rx_kernel (64 packets per wave)
+//                   the sizes); up to 64 K frames of <= 2 KiB slots 8 lanes per
+//                   packet; above, rx_kernel (64 packets per wave)
 // (since the select-form per-lane phase 2: 4 096 x 64 B quad 3.55 vs wave
 // 3.86 us, 2 048 x 64 B 3.53 vs 3.21; 8 192 x 1500 B wave 6.05 vs row 7.32,
 // 16 K 9.31 vs 7.35: profiles/r2/wave_probe_dispatch.jsonl; 128 K x 64 B quad 5.37
@@ -233,14 +234,22 @@ constexpr uint32_t kHeldPasses = 8;
 // (64 / 576 / 1500 B, 7 : 4 : 1) 77.8 vs 86.1 us; from 768 B slots on
 // rx_kernel is ahead again, 142.4 vs 146.4 us.)
 // Pointer bursts carry no size the host can see: they count as mid-size.
-// MTCP_GPU_SCHED=wave|row|quad|span|big at context open forces one kernel for
+// MTCP_GPU_SCHED=wave|row|quad|oct|span|big at context open forces one kernel for
 // every batch (A/B runs, and the parity tests of each); the tx fill of
 // pointer bursts and the tx report exist only in the small kernels, and the
 // span kernel is rx only (a forced span runs tx on rx_kernel).
-enum Sched : int { kSchedAuto = 0, kSchedWave, kSchedRow, kSchedQuad, kSchedBig, kSchedSpan };
+enum Sched : int { kSchedAuto = 0, kSchedWave, kSchedRow, kSchedQuad, kSchedBig, kSchedSpan, kSchedOct };
 
 constexpr uint64_t kQuadOnlyUpToSlot = 64;
 constexpr uint64_t kSpanUpToSlot = 640;
+// 32 K < n <= 64 K frames of 640 B < slot <= 2 KiB: 8-lane groups.  rx_kernel
+// fills half the GPU's wave slots at 64 K frames (1 024 waves of 64); through
+// the ABI, same frames and process, records identical (profiles/r4/oct_sweep.jsonl):
+// 64 K x 768 / 1024 / 1500 / 2048 B 8.8 / 11.8 / 17.3 / 21.3 us against
+// 16.9 / 17.3 / 19.8 / 32.4 (bimodal equal, 14.3 vs 14.2; 4 KiB slots and
+// 128 K frames of 1500 B keep rx_kernel).
+constexpr uint32_t kOctUpToPkts = 1u << 16;
+constexpr uint64_t kOctUpToSlot = 2048;
 
 int sched_from_env() {
     const char *e = getenv("MTCP_GPU_SCHED");
@@ -249,6 +258,7 @@ int sched_from_env() {
     if (!strcmp(e, "row")) return kSchedRow;
     if (!strcmp(e, "quad")) return kSchedQuad;
     if (!strcmp(e, "span")) return kSchedSpan;
+    if (!strcmp(e, "oct")) return kSchedOct;
     if (!strcmp(e, "big")) return kSchedBig;
     return kSchedAuto;
 }
@@ -257,7 +267,9 @@ int sched_from_env() {
 int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_only, bool rx) {
     int s = ctx->sched;
     if (s == kSchedAuto) {
-        const int big = slot <= kQuadOnlyUpToSlot ? kSchedQuad : slot <= kSpanUpToSlot ? kSchedSpan : kSchedBig;
+        const int big = slot <= kQuadOnlyUpToSlot ? kSchedQuad
+                        : slot <= kSpanUpToSlot   ? kSchedSpan
+                        : (n <= kOctUpToPkts && slot <= kOctUpToSlot) ? kSchedOct : kSchedBig;
         if (slot < 256) s = n <= 2048 ? kSchedWave : n <= (1u << 17) ? kSchedQuad : big;
         else if (slot > 4096) s = n <= (1u << 16) ? kSchedWave : kSchedBig;
         else s = n <= 8192 ? kSchedWave : n <= (1u << 15) ? kSchedRow : big;
@@ -290,6 +302,12 @@ const char *launch_small(int sched, uint32_t n, uint64_t slot, hipStream_t st, c
         hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 4, 0, 1, kBlk>), dim3((n + P - 1) / P), dim3(kBlk), 0,
                            st, kp);
         return "rx_group_kernel<quad>";
+    } else if (sched == kSchedOct) {
+        constexpr int kBlk = mg::kOctBlock;
+        constexpr uint32_t P = mg::GroupShape<8, kBlk>::P;
+        hipLaunchKernelGGL((mg::rx_group_kernel<MODE, RSS, 8, 0, 1, kBlk>), dim3((n + P - 1) / P), dim3(kBlk), 0,
+                           st, kp);
+        return "rx_group_kernel<oct>";
     } else if (sched == kSchedSpan) {
         if constexpr (!mg::is_tx(MODE)) {
             hipLaunchKernelGGL((mg::rx_span_kernel<MODE, RSS>), dim3((n + mg::kSpanP - 1) / mg::kSpanP),

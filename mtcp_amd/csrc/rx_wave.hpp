@@ -333,6 +333,8 @@ constexpr int kGroupBlock = 1024;              // 16 waves
 // profiles/r4/group_span_probe.jsonl).  Rows keep 1024: at 2-4 K MTU frames
 // the 256-thread rows lose (5.9 vs 4.2 us).
 constexpr int kQuadBlock = 256;
+// 8-lane groups (mid-size batches of MTU-class frames): 512 threads, P = 64
+constexpr int kOctBlock = 512;
 
 // BLK: threads per workgroup (P = BLK / G packets).  U: 16 B loads per lane
 // per trip (0: by G).

@@ -30,7 +30,7 @@ from tests.test_gpu_parity import DEV, to_dev
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-SCHEDS = ["wave", "row", "quad", "span", "big"]
+SCHEDS = ["wave", "row", "quad", "oct", "span", "big"]
 
 
 @pytest.fixture(scope="module")
@@ -100,9 +100,9 @@ def test_compact_golden_every_kernel(gpu, golden, monkeypatch, sched, rss):
         got_p = rx16(ctx, b, d, n, 0, ptrs=ptrs, bins=bins)
         bins_p = bins.cpu().numpy().view(np.uint32).copy()
     assert kernel, "mtcp_gpu_last_kernel names the dispatched kernel"
-    if sched in ("wave", "row", "quad", "span"):
-        assert kernel.startswith({"wave": "rx_wave", "row": "rx_group_kernel<row",
-                                  "quad": "rx_group_kernel<quad", "span": "rx_span_kernel"}[sched]), kernel
+    if sched in ("wave", "row", "quad", "oct", "span"):
+        assert kernel.startswith({"wave": "rx_wave", "row": "rx_group_kernel<row", "quad": "rx_group_kernel<quad",
+                                  "oct": "rx_group_kernel<oct", "span": "rx_span_kernel"}[sched]), kernel
     elif sched == "big":
         assert kernel.startswith("rx_kernel"), kernel
     for g, what in ((got, "chunk"), (got_f, "chunk+bins"), (got_p, "ptrs+bins")):

@@ -28,7 +28,7 @@ def gpu():
     return g
 
 
-SCHEDS = ["wave", "row", "quad", "span", "big"]
+SCHEDS = ["wave", "row", "quad", "oct", "span", "big"]
 
 
 @pytest.mark.parametrize("sched", SCHEDS)

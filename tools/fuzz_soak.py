@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fuzz soak (a checking tool, not product code): many seeds of the fuzz
 frames of tests/fuzz_frames.py through every kernel the library dispatches
-(MTCP_GPU_SCHED wave / row / quad / big), compared with the oracle field by
+(MTCP_GPU_SCHED wave / row / quad / oct / span / big), compared with the oracle field by
 field — rx over the chunk and over a pointer burst (40 B records, the RSS key
 and queue count drawn per seed), rx into 16 B records, and the tx fill byte
 for byte.  Prints a progress line every 10 seeds and one summary line.
@@ -21,7 +21,7 @@ from mtcp_amd import RESULT_DTYPE, RESULT16_DTYPE, compact_of, gpu  # noqa: E402
 from tests.fuzz_frames import fuzz_batch  # noqa: E402
 
 DEV = "cuda:0"
-SCHEDS = ("wave", "row", "quad", "big")
+SCHEDS = ("wave", "row", "quad", "oct", "span", "big")
 
 
 def to_dev(a):

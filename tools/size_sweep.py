@@ -5,8 +5,12 @@ in HBM, 50 back-to-back mtcp_gpu_rx_chunk_dev launches timed with HIP events
 on the launch stream, next to the box's read ceiling on the same buffer
 (tools/libstream_ceiling.so).  One JSON line per size: the kernel the
 dispatcher picked, its time, Σ L / t against 8 TB/s and against the stream.
-  usage: python tools/size_sweep.py [sizes...]"""
+  usage: python tools/size_sweep.py [--n N] [sizes...]
+  sizes: bytes, or "bimodal" (C3's 64 / 1500 B mix) or "imix" (64 / 576 /
+  1500 B, 7 : 4 : 1); --n fixes the batch (default ~1.5 GB of slots, <= 8 M).
+  MTCP_GPU_SCHED=wave|row|quad|oct|span|big forces a kernel (mtcp_gpu.hip)."""
 import ctypes
+import hashlib
 import json
 import os
 import sys
@@ -31,15 +35,26 @@ def ceiling_us(buf, nbytes, stream):
     return float(us.value)
 
 
+def lengths(n, size):
+    if size == "imix":
+        r = np.random.default_rng(5).integers(0, 12, n)
+        return np.where(r < 7, 64, np.where(r < 11, 576, 1500)).astype(np.uint16)
+    return pktgen.lengths(n, size if size == "bimodal" else int(size), 7)
+
+
 def main():
-    sizes = [int(a) for a in sys.argv[1:]] or SIZES
+    args = sys.argv[1:]
+    fixed_n = None
+    if args[:1] == ["--n"]:
+        fixed_n, args = int(args[1]), args[2:]
+    sizes = args or SIZES
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     for size in sizes:
-        slot = (size + 63) & ~63
-        n = min((3 << 29) // slot, 1 << 23)            # ~1.5 GB of slots, at most 8 M frames
-        desc, nbytes = pktgen.layout(n, size, 6, 7)
+        slot = 1600 if size in ("bimodal", "imix") else (int(size) + 63) & ~63
+        n = fixed_n or min((3 << 29) // slot, 1 << 23)   # ~1.5 GB of slots, at most 8 M frames
+        desc, nbytes = pktgen.layout_from_lengths(lengths(n, size), 6)
         buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         d = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
         out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
@@ -58,13 +73,17 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / reps
             kernel = ctx.last_kernel
+            got = out.clone()
         fb = int(desc["len"].astype(np.int64).sum())
-        print(json.dumps({"probe": "size_sweep", "frame_size": size, "frames": n, "kernel": kernel,
+        print(json.dumps({"probe": "size_sweep", "sched": os.environ.get("MTCP_GPU_SCHED", "auto"),
+                          "frame_size": size, "frames": n, "kernel": kernel,
                           "us_per_launch": round(us, 2), "GBs": round(fb / us / 1e3, 1),
                           "gpkt_per_s": round(n / us / 1e3, 3), "frac_of_8TBs": round(fb / us / 8e6, 4),
                           "ceiling_us": round(ceil, 2), "frac_of_ceiling": round(ceil / us, 4),
-                          "records_MB": round(n * 40 / 1e6, 1)}), flush=True)
-        del buf, d, out
+                          "records_MB": round(n * 40 / 1e6, 1),
+                          "records_sha": hashlib.sha256(got.cpu().numpy().tobytes()).hexdigest()[:16]}),
+              flush=True)
+        del buf, d, out, got
         torch.cuda.empty_cache()
 
 
