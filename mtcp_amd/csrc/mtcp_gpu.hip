@@ -217,7 +217,10 @@ constexpr uint32_t kHeldPasses = 8;
 // tools/wave_probe.hip and tools/small_batch_probe.py (same frames, same
 // process):
 //   slot < 256 B:   n <= 2 048  wave;  n <= 128 K a quad per packet (64 per workgroup)
-//   slot > 4 KiB:   n <= 64 K   wave (a jumbo frame in one trip)
+//   slot >= 4 KiB:  n <= 64 K   wave (a jumbo frame in one trip; 4 KiB slots
+//                   since round 4: 16 K / 32 K / 64 K frames 11.8 / 21.1 / 40.4 us
+//                   against the row kernel's 16.1 / 27.6 and rx_kernel's 51.6,
+//                   profiles/r4/dispatch_map.jsonl)
 //   otherwise:      n <= 8 192  wave;  n <= 32 K  a row per packet (64 per workgroup)
 //   larger batches: slot <= 64 B a quad per packet; slot <= 640 B rx_span_kernel
 //                   (rx_span.hpp: the workgroup's chunks back to back, whatever
@@ -271,7 +274,7 @@ int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_on
                         : slot <= kSpanUpToSlot   ? kSchedSpan
                         : (n <= kOctUpToPkts && slot <= kOctUpToSlot) ? kSchedOct : kSchedBig;
         if (slot < 256) s = n <= 2048 ? kSchedWave : n <= (1u << 17) ? kSchedQuad : big;
-        else if (slot > 4096) s = n <= (1u << 16) ? kSchedWave : kSchedBig;
+        else if (slot >= 4096) s = n <= (1u << 16) ? kSchedWave : kSchedBig;
         else s = n <= 8192 ? kSchedWave : n <= (1u << 15) ? kSchedRow : big;
     }
     if (s == kSchedSpan && !rx) s = kSchedBig;

@@ -14,7 +14,8 @@
 //                   chunk is <= j: a 6-step binary search over the 64 starts,
 //                   each step a ds_bpermute of the lane that holds them (a
 //                   frame with no chunks shares its start with the next one,
-//                   and the search takes the larger index, so it is skipped)
+//                   and the search takes the larger index, so it is skipped);
+//                   a tile whose 64 frames have one chunk count divides instead
 //   sums            v_sad_u16 over the chunk, an inclusive scan over the
 //                   wave; the last lane of each frame's run in the window
 //                   adds the run's sum (scan minus the scan before the run)
@@ -123,6 +124,10 @@ __global__ __launch_bounds__(kSpanBlock) void rx_span_kernel(KParams kp) {
     }
 
     // ---- the chunk stream ----------------------------------------------------------
+    // A tile of 64 frames of one chunk count (fixed-size traffic) needs no
+    // search: frame j / nch, chunk j % nch.
+    const uint32_t nch0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)nch);
+    const bool uniform = nch0 != 0 && __ballot(nch != nch0) == 0;
     for (uint32_t base = wib * kWave; base < C; base += kStride * U) {      // wave-uniform
         v4u x[U];
         uint32_t qv[U], cv[U];
@@ -131,8 +136,13 @@ __global__ __launch_bounds__(kSpanBlock) void rx_span_kernel(KParams kp) {
             const uint32_t j0 = base + u * kStride;
             if (j0 < C) {
                 const uint32_t j = min(j0 + lane, C - 1);               // past the end: a valid chunk, unused
-                uint32_t s;
-                const uint32_t q = span_find(start, j, &s);
+                uint32_t s, q;
+                if (uniform) {
+                    q = j / nch0;
+                    s = q * nch0;
+                } else {
+                    q = span_find(start, j, &s);
+                }
                 qv[u] = q;
                 cv[u] = j - s;
                 const uint64_t fq = ((uint64_t)shfl32(p16hi, (int)q) << 32) | shfl32(p16lo, (int)q);

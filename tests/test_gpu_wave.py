@@ -115,15 +115,17 @@ def imix_lengths(n, seed):
     ((1 << 17) + 1, 64, "rx_group_kernel<quad"), ((1 << 17) + 1, 128, "rx_span_kernel"),
     (8192, 1500, "rx_wave"), (8193, 1500, "rx_group_kernel<row"), (32768, 512, "rx_group_kernel<row"),
     (32769, 512, "rx_span_kernel"), (32769, 640, "rx_span_kernel"), (32769, 704, "rx_group_kernel<oct"),
-    (65536, 1500, "rx_group_kernel<oct"), (65537, 1500, "rx_kernel"), (65536, 4096, "rx_kernel"),
+    (65536, 1500, "rx_group_kernel<oct"), (65537, 1500, "rx_kernel"), (65536, 4096, "rx_wave"),
+    (65537, 4096, "rx_kernel"), (16384, 4032, "rx_group_kernel<row"),
     ((1 << 18) + 3, "imix", "rx_span_kernel")])
 def test_dispatch_boundaries(gpu, monkeypatch, n, size, kernel):
     """The automatic kernel choice (mtcp_gpu.hip pick_sched) on both sides of
     each boundary it draws — small frames: wave up to 2 048, quad up to
     128 K, then quads for 64 B slots and the span kernel for larger ones; MTU
     frames: wave up to 8 192, row up to 32 K, 8 lanes per packet up to 64 K
-    (slots <= 2 KiB), rx_kernel above; past 32 K frames of <= 640 B slots the
-    span kernel — each the kernel it should be, and equal to the oracle."""
+    (slots <= 2 KiB), rx_kernel above; 4 KiB slots and up: wave up to 64 K;
+    past 32 K frames of <= 640 B slots the span kernel — each the kernel it
+    should be, and equal to the oracle."""
     monkeypatch.delenv("MTCP_GPU_SCHED", raising=False)
     seed = 67
     if size == "imix":

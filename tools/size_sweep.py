@@ -5,7 +5,7 @@ in HBM, 50 back-to-back mtcp_gpu_rx_chunk_dev launches timed with HIP events
 on the launch stream, next to the box's read ceiling on the same buffer
 (tools/libstream_ceiling.so).  One JSON line per size: the kernel the
 dispatcher picked, its time, Σ L / t against 8 TB/s and against the stream.
-  usage: python tools/size_sweep.py [--n N] [sizes...]
+  usage: python tools/size_sweep.py [--n N] [--no-ceiling] [sizes...]
   sizes: bytes, or "bimodal" (C3's 64 / 1500 B mix) or "imix" (64 / 576 /
   1500 B, 7 : 4 : 1); --n fixes the batch (default ~1.5 GB of slots, <= 8 M).
   MTCP_GPU_SCHED=wave|row|quad|oct|span|big forces a kernel (mtcp_gpu.hip)."""
@@ -44,9 +44,12 @@ def lengths(n, size):
 
 def main():
     args = sys.argv[1:]
-    fixed_n = None
-    if args[:1] == ["--n"]:
-        fixed_n, args = int(args[1]), args[2:]
+    fixed_n, ceiling = None, True
+    while args[:1] in (["--n"], ["--no-ceiling"]):
+        if args[0] == "--n":
+            fixed_n, args = int(args[1]), args[2:]
+        else:
+            ceiling, args = False, args[1:]
     sizes = args or SIZES
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
@@ -60,7 +63,7 @@ def main():
         out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
         gpu.pktgen_dev(buf, d, n, 6, 7, stream=stream)
         with gpu.Context(0) as ctx:
-            ceil = ceiling_us(buf, nbytes, stream)
+            ceil = ceiling_us(buf, nbytes, stream) if ceiling else float("nan")
             for _ in range(5):
                 ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream)
             torch.cuda.synchronize()
