@@ -71,7 +71,7 @@ def test_fuzz_tx_fill_matches_oracle(gpu, seed, aligned, sched, monkeypatch):
     assert np.array_equal(host, want)
 
 
-@pytest.mark.parametrize("sched", ["wave", "row", "quad"])
+@pytest.mark.parametrize("sched", ["wave", "row", "quad", "oct"])
 def test_fuzz_tx_fill_ptrs_matches_oracle(gpu, sched, monkeypatch):
     """The pointer-burst tx fill (host frames: staged, filled, check fields
     written back; device frames: filled in place) on the fuzz frames."""

@@ -315,7 +315,7 @@ def test_fused_flow_bins_equal_separate_pass(gpu, size, n):
     assert (bins.cpu().numpy().view(np.uint32) != 0xFFFFFFFF).mean() > 0.99
 
 
-@pytest.mark.parametrize("sched", ["wave", "row", "quad"])
+@pytest.mark.parametrize("sched", ["wave", "row", "quad", "oct"])
 def test_tx_fill_ptrs_golden(gpu, golden, monkeypatch, sched):
     """mtcp_gpu_tx_fill_ptrs (host frames, e.g. a DPDK m_table burst) and
     _dev (device-accessible frames): exactly the reference's fills, and only
