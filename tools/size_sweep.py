@@ -5,7 +5,8 @@ in HBM, 50 back-to-back mtcp_gpu_rx_chunk_dev launches timed with HIP events
 on the launch stream, next to the box's read ceiling on the same buffer
 (tools/libstream_ceiling.so).  One JSON line per size: the kernel the
 dispatcher picked, its time, Σ L / t against 8 TB/s and against the stream.
-  usage: python tools/size_sweep.py [--n N] [--no-ceiling] [sizes...]
+  usage: python tools/size_sweep.py [--n N] [--no-ceiling] [--ptrs] [sizes...]
+  --ptrs: the same frames as a pointer burst (mtcp_gpu_rx_ptrs_dev).
   sizes: bytes, or "bimodal" (C3's 64 / 1500 B mix) or "imix" (64 / 576 /
   1500 B, 7 : 4 : 1); --n fixes the batch (default ~1.5 GB of slots, <= 8 M).
   MTCP_GPU_SCHED=wave|row|quad|oct|span|big forces a kernel (mtcp_gpu.hip)."""
@@ -44,10 +45,12 @@ def lengths(n, size):
 
 def main():
     args = sys.argv[1:]
-    fixed_n, ceiling = None, True
-    while args[:1] in (["--n"], ["--no-ceiling"]):
+    fixed_n, ceiling, ptrs = None, True, False
+    while args[:1] in (["--n"], ["--no-ceiling"], ["--ptrs"]):
         if args[0] == "--n":
             fixed_n, args = int(args[1]), args[2:]
+        elif args[0] == "--ptrs":
+            ptrs, args = True, args[1:]
         else:
             ceiling, args = False, args[1:]
     sizes = args or SIZES
@@ -62,23 +65,30 @@ def main():
         d = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
         out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
         gpu.pktgen_dev(buf, d, n, 6, 7, stream=stream)
+        if ptrs:
+            p = torch.from_numpy((desc["offset"].astype(np.int64) << 6) + buf.data_ptr()).to(dev)
+            ln = torch.from_numpy(desc["len"].view(np.int16).copy()).to(dev)
+            launch = lambda ctx: ctx.rx_ptrs_dev(p, ln, n, out, stream=stream)  # noqa: E731
+        else:
+            launch = lambda ctx: ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream)  # noqa: E731
         with gpu.Context(0) as ctx:
             ceil = ceiling_us(buf, nbytes, stream) if ceiling else float("nan")
             for _ in range(5):
-                ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream)
+                launch(ctx)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             reps = 50
             e0.record(stream)
             for _ in range(reps):
-                ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream)
+                launch(ctx)
             e1.record(stream)
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / reps
             kernel = ctx.last_kernel
             got = out.clone()
         fb = int(desc["len"].astype(np.int64).sum())
-        print(json.dumps({"probe": "size_sweep", "sched": os.environ.get("MTCP_GPU_SCHED", "auto"),
+        print(json.dumps({"probe": "size_sweep", "mode": "ptrs" if ptrs else "chunk",
+                          "sched": os.environ.get("MTCP_GPU_SCHED", "auto"),
                           "frame_size": size, "frames": n, "kernel": kernel,
                           "us_per_launch": round(us, 2), "GBs": round(fb / us / 1e3, 1),
                           "gpkt_per_s": round(n / us / 1e3, 3), "frac_of_8TBs": round(fb / us / 8e6, 4),
