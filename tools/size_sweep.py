@@ -5,8 +5,9 @@ in HBM, 50 back-to-back mtcp_gpu_rx_chunk_dev launches timed with HIP events
 on the launch stream, next to the box's read ceiling on the same buffer
 (tools/libstream_ceiling.so).  One JSON line per size: the kernel the
 dispatcher picked, its time, Σ L / t against 8 TB/s and against the stream.
-  usage: python tools/size_sweep.py [--n N] [--no-ceiling] [--ptrs] [sizes...]
+  usage: python tools/size_sweep.py [--n N] [--no-ceiling] [--ptrs] [--compact] [sizes...]
   --ptrs: the same frames as a pointer burst (mtcp_gpu_rx_ptrs_dev).
+  --compact: 16 B records (MTCP_GPU_F_COMPACT) instead of 40 B.
   sizes: bytes, or "bimodal" (C3's 64 / 1500 B mix) or "imix" (64 / 576 /
   1500 B, 7 : 4 : 1); --n fixes the batch (default ~1.5 GB of slots, <= 8 M).
   MTCP_GPU_SCHED=wave|row|quad|oct|span|big forces a kernel (mtcp_gpu.hip)."""
@@ -45,12 +46,14 @@ def lengths(n, size):
 
 def main():
     args = sys.argv[1:]
-    fixed_n, ceiling, ptrs = None, True, False
-    while args[:1] in (["--n"], ["--no-ceiling"], ["--ptrs"]):
+    fixed_n, ceiling, ptrs, compact = None, True, False, False
+    while args[:1] in (["--n"], ["--no-ceiling"], ["--ptrs"], ["--compact"]):
         if args[0] == "--n":
             fixed_n, args = int(args[1]), args[2:]
         elif args[0] == "--ptrs":
             ptrs, args = True, args[1:]
+        elif args[0] == "--compact":
+            compact, args = True, args[1:]
         else:
             ceiling, args = False, args[1:]
     sizes = args or SIZES
@@ -63,7 +66,8 @@ def main():
         desc, nbytes = pktgen.layout_from_lengths(lengths(n, size), 6)
         buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         d = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
-        out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+        rec = 16 if compact else 40
+        out = torch.empty(n * rec, dtype=torch.uint8, device=dev)
         gpu.pktgen_dev(buf, d, n, 6, 7, stream=stream)
         if ptrs:
             p = torch.from_numpy((desc["offset"].astype(np.int64) << 6) + buf.data_ptr()).to(dev)
@@ -71,7 +75,7 @@ def main():
             launch = lambda ctx: ctx.rx_ptrs_dev(p, ln, n, out, stream=stream)  # noqa: E731
         else:
             launch = lambda ctx: ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream)  # noqa: E731
-        with gpu.Context(0) as ctx:
+        with gpu.Context(0, compact=compact) as ctx:
             ceil = ceiling_us(buf, nbytes, stream) if ceiling else float("nan")
             for _ in range(5):
                 launch(ctx)
@@ -93,7 +97,7 @@ def main():
                           "us_per_launch": round(us, 2), "GBs": round(fb / us / 1e3, 1),
                           "gpkt_per_s": round(n / us / 1e3, 3), "frac_of_8TBs": round(fb / us / 8e6, 4),
                           "ceiling_us": round(ceil, 2), "frac_of_ceiling": round(ceil / us, 4),
-                          "records_MB": round(n * 40 / 1e6, 1),
+                          "records_MB": round(n * rec / 1e6, 1),
                           "records_sha": hashlib.sha256(got.cpu().numpy().tobytes()).hexdigest()[:16]}),
               flush=True)
         del buf, d, out, got
