@@ -29,7 +29,7 @@ golden:
 	$(MAKE) -C oracle golden
 
 clean:
-	rm -f $(LIB)
+	rm -f $(LIB) tests/c/libmtcp_gpu_testing.so tests/c/rxloop tests/c/admit_test tools/libstream_ceiling.so
 	$(MAKE) -C oracle clean
 
 # the probe tools instantiate rx_kernel's profiling / timing-probe variants

@@ -39,8 +39,11 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import sys
 import time
+
+T_START = time.perf_counter()
 
 import numpy as np
 import torch
@@ -157,6 +160,10 @@ def parse():
     ap.add_argument("--numa", default="on", choices=["on", "off"],
                     help="run each rank on the cpus local to its GPU (sysfs local_cpulist), so the "
                          "host buffers of the CPU-baseline and PCIe-inclusive legs sit on its socket")
+    ap.add_argument("--c4-per-gpu", default="auto", choices=["auto", "on", "off"],
+                    help="N = 1: also time C4's per-GPU step (2 M x 1500 B, two launches; what each "
+                         "rank of `--gpus N` runs) in the same run, so that the 1 -> N ratio can "
+                         "compare identical per-GPU work (auto: on for the default C2 line)")
     ap.add_argument("--record", default="full", choices=["full", "compact"],
                     help="rx result record: the 40 B mtcp_gpu_result (default, the headline) or "
                          "the 16 B mtcp_gpu_result16 of a MTCP_GPU_F_COMPACT context")
@@ -242,6 +249,27 @@ def read_ceiling(d_buf, nbytes, stream, reps=20):
     us, shape = ctypes.c_float(0.0), ctypes.c_int(0)
     if f(d_buf.data_ptr(), nbytes, reps, stream.cuda_stream, ctypes.byref(us), ctypes.byref(shape)) != 0:
         raise RuntimeError("stream_ceiling_us failed")
+    return float(us.value), int(shape.value)
+
+
+def patch_ceiling(d_buf, d_desc, n, stream, reps=20):
+    """The f1 row's ceiling, measured now on its own frames: the tx fill's
+    access pattern without its arithmetic (read every frame, write the two
+    u16 check fields of each, the bytes unchanged), fastest of four shapes,
+    tools/stream_ceiling.hip patch_walk.  None when the probe library is not
+    built."""
+    import ctypes
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "libstream_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    f = ctypes.CDLL(path).patch_ceiling_us
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                  ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    f.restype = ctypes.c_int
+    us, shape = ctypes.c_float(0.0), ctypes.c_int(0)
+    if f(d_buf.data_ptr(), d_desc.data_ptr(), n, 6, reps, stream.cuda_stream, ctypes.byref(us),
+         ctypes.byref(shape)) != 0:
+        raise RuntimeError("patch_ceiling_us failed")
     return float(us.value), int(shape.value)
 
 
@@ -473,6 +501,42 @@ def _timed(step, steps, warmup, stream):
     return (time.perf_counter() - t0) / steps, ev0.elapsed_time(ev1) / steps / 1e3
 
 
+def c4_per_gpu(ctx, dev, stream, steps, warmup):
+    """C4's per-GPU step on this one GPU, in the N = 1 run: the 2 M x 1500 B
+    shard rank 0 of `bench.py --gpus 8` processes (frames 0 .. 2 M of C4's
+    seed-4 stream, byte-identical to that rank's shard), timed exactly as the
+    N > 1 ranks time it — one mtcp_gpu_rx_chunk_dev call per step (two
+    launches of 1 M, mtcp_gpu.hip kHeldPasses), K direct calls between HIP
+    events on the launch stream.  Value / N-GPU line's value / N is then the
+    scaling of identical per-GPU work."""
+    from mtcp_amd import _lib, gpu
+    cfg = CONFIGS["c4"]
+    sh = shard.make_shard(cfg["per_gpu"], cfg["size"], 0, 1, cfg["seed"])
+    d_buf = torch.empty(sh.nbytes, dtype=torch.uint8, device=dev)
+    d_desc = torch.from_numpy(sh.desc.view(np.uint8).copy()).to(dev)
+    d_out = torch.empty(sh.count * 40, dtype=torch.uint8, device=dev)
+    gpu.pktgen_dev(d_buf, d_desc, sh.count, 6, cfg["seed"], sh.first_index, stream=stream)
+    frame_bytes = int(sh.desc["len"].astype(np.int64).sum())
+    rx_fn = _lib.lib().mtcp_gpu_rx_chunk_dev
+    rx_args = (ctx._h, d_buf.data_ptr(), sh.nbytes, d_desc.data_ptr(), sh.count, 6, d_out.data_ptr(),
+               stream.cuda_stream)
+    rcs = []
+    wall, kern = _timed(lambda: rcs.append(rx_fn(*rx_args)), steps, warmup, stream)
+    if any(rc != 0 for rc in rcs):
+        raise RuntimeError(f"mtcp_gpu_rx_chunk_dev failed ({[rc for rc in rcs if rc][0]})")
+    ok = float((d_out.view(-1, 40)[:, 36] == 0).float().mean())
+    del d_buf, d_desc, d_out
+    torch.cuda.empty_cache()
+    return {"value": round(frame_bytes / wall / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(wall * 1e3, 5), "gpkt_per_s": round(sh.count / wall / 1e9, 4),
+            "packets": sh.count, "frame_bytes": frame_bytes, "launches_per_step": 2,
+            "kernel": "mg::" + ctx.last_kernel, "avg_step_ms_events": round(kern * 1e3, 5),
+            "frac": round(frame_bytes / kern / 1e9 / HBM_PEAK_GBS, 4), "tcp_ok_fraction": round(ok, 5),
+            "note": "C4's per-GPU step (rank 0's 2 M x 1500 B shard of the 16 M batch) on this GPU in "
+                    "the same run, timed as each rank of --gpus N times it: the N-GPU line's value "
+                    "/ N / this value is the scaling of identical per-GPU work"}
+
+
 def _cpu_time(fn, reps=3):
     best = None
     for _ in range(reps):
@@ -509,6 +573,12 @@ def run_row(args):
     if args.config == "f1":
         # idempotent after the first fill: every step rewrites the same checks
         step = lambda: ctx.tx_fill_dev(d_buf, d_desc, n, 6, stream=stream)
+        # the access pattern's own ceiling on these frames, measured now,
+        # before the fill's launches (as read_ceiling is for rx)
+        try:
+            ceil = patch_ceiling(d_buf, d_desc, n, stream)
+        except Exception as exc:      # never costs the line
+            ceil = repr(exc)
         wall, kern = _timed(step, args.steps, args.warmup, stream)
         algo = frame_bytes + 4 * n
         line.update(value=round(frame_bytes / wall / 1e9, 2), unit="GB/s", dtype="u8",
@@ -522,16 +592,20 @@ def run_row(args):
                             "avg_launch_ms": round(kern * 1e3, 5),
                             "algorithmic_bytes_per_launch": algo,
                             "note": "sum L read + 4 B of check fields written per frame"}
-        # the access pattern's own ceiling: one 2 x 2-byte patch per 1536 B
-        # slot costs a 32 B write granule and a dirty sector per frame
-        # (DESIGN §7), measured by tools/store_probe.hip slot_patch
-        cj = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "ceilings.json")
-        if os.path.exists(cj):
-            c = json.load(open(cj)).get("f1")
-            if c:
-                line["roofline"]["ceiling_us"] = c["us_per_launch"]
-                line["roofline"]["ceiling_frac"] = round(c["us_per_launch"] / (kern * 1e6), 4)
-                line["roofline"]["ceiling_source"] = c["source"]
+        # the access pattern's own ceiling: a 2 x 2-byte patch per frame
+        # costs a write granule and a dirty sector per frame,
+        # measured in this run on these frames (tools/stream_ceiling.hip)
+        if isinstance(ceil, tuple):
+            cus, shape = ceil
+            line["roofline"]["ceiling"] = {
+                "us": round(cus, 2), "kernel_frac_of_ceiling": round(cus / (kern * 1e6), 4),
+                "what": f"the fill's access pattern without its arithmetic on the same {n} frames: each "
+                        f"16-lane row reads its frame ({shape // 10} loads per lane), lanes 1 and 3 write "
+                        f"the u16 at bytes 24 and 50 back (values unchanged); fastest of 4 shapes "
+                        f"({shape % 10} WG/CU won), 20 launches, HIP events, measured before the fill; "
+                        f"tools/stream_ceiling.hip patch_walk"}
+        elif ceil is not None:
+            line["roofline"]["ceiling"] = {"error": ceil}
         if want_cpu:
             import oracle   # test infrastructure: the baseline leg only
             host = d_buf.cpu().numpy()
@@ -867,6 +941,13 @@ def main():
             if rank == 0:
                 extra["cpu_baseline"] = cb
         del host
+    want_c4 = args.c4_per_gpu == "on" or (args.c4_per_gpu == "auto" and world == 1 and args.config == "c2"
+                                          and not args.per_gpu and not compact)
+    if world == 1 and want_c4:
+        try:
+            extra["c4_per_gpu"] = c4_per_gpu(ctx, dev, stream, args.steps, args.warmup)
+        except Exception as exc:      # never costs the headline line
+            extra["c4_per_gpu"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and args.small_batch != "off":
         try:
             extra["small_batch"] = small_batch(ctx, dev, stream)
@@ -878,6 +959,14 @@ def main():
                                                  int(hdesc["len"].astype(np.int64).sum()), world)
         del host
     ctx.close()
+
+    # the run's own footprint (the 8-GPU default run's wall time
+    # and host memory): wall seconds from process start, peak host RSS, the
+    # max over ranks
+    run = torch.tensor([time.perf_counter() - T_START,
+                        resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(run, op=dist.ReduceOp.MAX)
 
     if rank == 0:
         # per-GPU roofline of the slowest rank's launches (N > 1: the max
@@ -911,6 +1000,9 @@ def main():
                          "algorithmic_bytes_per_launch": frame_bytes},
             "tcp_ok_fraction": round(ok_frac, 5),
             "host_cpus": host_cpus,
+            "run": {"wall_s_max_rank": round(float(run[0]), 1), "host_rss_gb_max_rank": round(float(run[1]), 2),
+                    "note": "each rank's seconds from its start to the end of its legs and its peak "
+                            "resident host memory, the max over ranks"},
         }
         if isinstance(ceiling, tuple):
             cus, shape = ceiling

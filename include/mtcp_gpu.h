@@ -70,8 +70,10 @@
 extern "C" {
 #endif
 
-#define MTCP_GPU_ABI_VERSION 3   /* 2: MTCP_GPU_F_COMPACT, mtcp_gpu_result16;
-                                    3: mtcp_gpu_rxq_get16, mtcp_gpu_debug_stall moved to the test library */
+#define MTCP_GPU_ABI_VERSION 4   /* 2: MTCP_GPU_F_COMPACT, mtcp_gpu_result16;
+                                    3: mtcp_gpu_rxq_get16, mtcp_gpu_debug_stall moved to the test library;
+                                    4: mtcp_gpu_tx_fill_ptrs_for, mtcp_gpu_host_stream,
+                                       mtcp_gpu_size_hint, mtcp_gpu_rx_chunk_hint_dev */
 
 /* ---- error codes (negative returns) ----------------------------------- */
 #define MTCP_GPU_OK        0
@@ -233,6 +235,11 @@ int  mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp);
 /* The HIP stream the context launches on (a hipStream_t, as void*). */
 void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx);
 
+/* The HIP stream the host-memory calls (mtcp_gpu_rx_chunk's first stage,
+ * _rx_ptrs, _tx_fill, _tx_fill_ptrs[_for], _flow_hash) run on, created on
+ * first use; NULL if it cannot be created or the context was abandoned. */
+void *mtcp_gpu_host_stream(mtcp_gpu_ctx *ctx);
+
 /* Bytes per rx result record this context writes: 40, or 16 with
  * MTCP_GPU_F_COMPACT; 0 for a NULL context. */
 uint32_t mtcp_gpu_record_size(const mtcp_gpu_ctx *ctx);
@@ -277,6 +284,30 @@ int mtcp_gpu_rx_chunk_flow_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t bu
 int mtcp_gpu_rx_ptrs_flow_dev(mtcp_gpu_ctx *ctx, const uint8_t *const *d_pkts,
                               const uint16_t *d_lens, uint32_t n,
                               mtcp_gpu_result *d_out, uint32_t *d_bins, void *stream);
+
+/*
+ * What the caller knows of a batch's frame lengths, for the choice of kernel:
+ * the smallest and the largest non-zero frame length in it.  The device
+ * entry points above cannot see the lengths (the descriptors are in device
+ * memory) and choose by the batch's average slot (buf_len / n) alone, which
+ * cannot tell a uniform batch of 768 B frames from a 64 / 1500 B mix of the
+ * same average.  An io_module sees every length as it stages a frame
+ * (mtcp_gpu_rxq_push, as RunMainLoop's get_rptr hands it over, core.c:771):
+ * with the hint, a batch whose 64 B slots all lie within 2x of each other
+ * takes the kernel measured fastest for uniform batches of that size.  The
+ * records are the same with or without a hint, and for any hint; the host
+ * rx calls (mtcp_gpu_rx_chunk, _rx_ptrs) and the rxqs derive it themselves.
+ */
+typedef struct mtcp_gpu_size_hint {
+    uint16_t min_len;
+    uint16_t max_len;
+} mtcp_gpu_size_hint;
+
+/* mtcp_gpu_rx_chunk_flow_dev with a size hint (NULL: exactly that call). */
+int mtcp_gpu_rx_chunk_hint_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
+                               const mtcp_gpu_desc *d_desc, uint32_t n,
+                               uint32_t off_shift, mtcp_gpu_result *d_out,
+                               uint32_t *d_bins, const mtcp_gpu_size_hint *hint, void *stream);
 
 /*
  * Host-memory rx (the drop-in for the rx loop): chunk and descriptors in host
@@ -324,6 +355,21 @@ int mtcp_gpu_tx_fill_ptrs_dev(mtcp_gpu_ctx *ctx, uint8_t *const *d_pkts,
                               const uint16_t *d_lens, uint32_t n, void *stream);
 int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_t *lens,
                           uint32_t n, uint32_t *n_filled);
+
+/*
+ * mtcp_gpu_tx_fill_ptrs with a bound on the wait (timeout_us 0: none, exactly
+ * mtcp_gpu_tx_fill_ptrs).  If the GPU has not reported within timeout_us,
+ * nothing has been written into the caller's frames, MTCP_GPU_ETIMEDOUT is
+ * returned, and the context is ABANDONED: the copies it gave up on may still
+ * run into its staging, so every later call on it answers MTCP_GPU_EIO
+ * without touching the device, and mtcp_gpu_close frees only its host-side
+ * state (its streams and buffers stay allocated).  The caller fills the
+ * frames itself, as mTCP does when dev_ioctl answers -1 (tcp_out.c:320-329,
+ * ip_out.c:147-165): an io_module's send_pkts (core.c:818-824) never blocks
+ * on a GPU that stopped answering.
+ */
+int mtcp_gpu_tx_fill_ptrs_for(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_t *lens,
+                              uint32_t n, uint32_t *n_filled, uint32_t timeout_us);
 
 /* ---- flow-table hash (HashFlow) --------------------------------------- */
 #define MTCP_GPU_NUM_BINS_FLOWS  131072u      /* mtcp/src/include/fhash.h:7 */

@@ -15,11 +15,12 @@ LIB_PATH = os.path.join(HERE, "lib", "libmtcp_gpu.so")
 EXPORTS = (
     "mtcp_gpu_abi_version", "mtcp_gpu_strerror", "mtcp_gpu_device_count", "mtcp_gpu_device_pci_bus_id",
     "mtcp_gpu_open",
-    "mtcp_gpu_close", "mtcp_gpu_reserve", "mtcp_gpu_dev_ioctl", "mtcp_gpu_stream",
+    "mtcp_gpu_close", "mtcp_gpu_reserve", "mtcp_gpu_dev_ioctl", "mtcp_gpu_stream", "mtcp_gpu_host_stream",
     "mtcp_gpu_record_size", "mtcp_gpu_last_kernel", "mtcp_gpu_rx_chunk_dev",
     "mtcp_gpu_rx_ptrs_dev", "mtcp_gpu_rx_chunk", "mtcp_gpu_rx_ptrs", "mtcp_gpu_tx_fill_dev",
-    "mtcp_gpu_tx_fill", "mtcp_gpu_rx_chunk_flow_dev", "mtcp_gpu_rx_ptrs_flow_dev",
-    "mtcp_gpu_tx_fill_ptrs_dev", "mtcp_gpu_tx_fill_ptrs", "mtcp_gpu_host_register", "mtcp_gpu_host_unregister", "mtcp_gpu_sync",
+    "mtcp_gpu_tx_fill", "mtcp_gpu_rx_chunk_flow_dev", "mtcp_gpu_rx_ptrs_flow_dev", "mtcp_gpu_rx_chunk_hint_dev",
+    "mtcp_gpu_tx_fill_ptrs_dev", "mtcp_gpu_tx_fill_ptrs", "mtcp_gpu_tx_fill_ptrs_for",
+    "mtcp_gpu_host_register", "mtcp_gpu_host_unregister", "mtcp_gpu_sync",
     "mtcp_gpu_flow_hash_dev", "mtcp_gpu_flow_hash", "mtcp_gpu_rss_queue_map_dev",
     "mtcp_gpu_addr_pool_search", "mtcp_gpu_pktgen_dev",
     "mtcp_gpu_rxq_create", "mtcp_gpu_rxq_destroy", "mtcp_gpu_rxq_push", "mtcp_gpu_rxq_push_chunk",
@@ -57,6 +58,7 @@ def lib() -> ctypes.CDLL:
         "mtcp_gpu_reserve": ([vp, u64, u32], i32),
         "mtcp_gpu_dev_ioctl": ([vp, i32, i32, vp], i32),
         "mtcp_gpu_stream": ([vp], vp),
+        "mtcp_gpu_host_stream": ([vp], vp),
         "mtcp_gpu_record_size": ([vp], u32),
         "mtcp_gpu_last_kernel": ([vp], ctypes.c_char_p),
         "mtcp_gpu_sync": ([vp], i32),
@@ -68,8 +70,10 @@ def lib() -> ctypes.CDLL:
         "mtcp_gpu_tx_fill": ([vp, vp, u64, vp, u32, u32, ctypes.POINTER(u32)], i32),
         "mtcp_gpu_rx_chunk_flow_dev": ([vp, vp, u64, vp, u32, u32, vp, vp, vp], i32),
         "mtcp_gpu_rx_ptrs_flow_dev": ([vp, vp, u16p, u32, vp, vp, vp], i32),
+        "mtcp_gpu_rx_chunk_hint_dev": ([vp, vp, u64, vp, u32, u32, vp, vp, vp, vp], i32),
         "mtcp_gpu_tx_fill_ptrs_dev": ([vp, vp, u16p, u32, vp], i32),
         "mtcp_gpu_tx_fill_ptrs": ([vp, vp, u16p, u32, ctypes.POINTER(u32)], i32),
+        "mtcp_gpu_tx_fill_ptrs_for": ([vp, vp, u16p, u32, ctypes.POINTER(u32), u32], i32),
         "mtcp_gpu_host_register": ([vp, u64], i32),
         "mtcp_gpu_host_unregister": ([vp], i32),
         "mtcp_gpu_flow_hash_dev": ([vp, vp, u32, vp, vp], i32),

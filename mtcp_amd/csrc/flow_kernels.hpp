@@ -83,6 +83,9 @@ struct PoolParams {
 // consecutive candidates, a lane four of them, so every dword store of a
 // wave is 256 contiguous bytes.
 constexpr uint32_t kQmapTile = 4 * 4 * kBlock;     // 4096 candidates per workgroup
+// rss_queue_map_kernel fills its 256-entry nibble tables one entry per lane
+// and walks a tile in passes of 4 x 256 candidates (1024u * k below)
+static_assert(kBlock == 256, "rss_queue_map_kernel's table fill and pass stride assume 256 lanes");
 
 __device__ __forceinline__ uint32_t toeplitz_fixed7(const uint32_t *tab, uint32_t sip, uint32_t dip,
                                                     uint32_t dport) {

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 
 #include "../../include/mtcp_gpu.h"
@@ -54,6 +55,11 @@ struct mtcp_gpu_ctx {
     mtcp_gpu_desc *h_gather_desc = nullptr;
     uint32_t h_gather_desc_cap = 0;
     const char *last_kernel = "";                // mtcp_gpu_last_kernel
+    hipEvent_t done_evt = nullptr;               // completion of a bounded host call
+    // a host call's bounded wait gave up (mtcp_gpu_tx_fill_ptrs_for): work of
+    // that call may still read or write the staging, so nothing is issued,
+    // staged or freed on this context again (every call answers EIO)
+    bool abandoned = false;
 };
 
 namespace {
@@ -266,16 +272,52 @@ int sched_from_env() {
     return kSchedAuto;
 }
 
-// rx: the batch is an rx launch (the span kernel exists for rx only)
-int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_only, bool rx) {
+// A batch known to be of one size class (mtcp_gpu_size_hint: every 64 B
+// slot within 2x of the smallest) takes the kernels measured fastest on
+// uniform batches where those differ from the choice for mixes of the same
+// average slot (profiles/r4/dispatch_map_final.jsonl, same process, records
+// identical): 64 K frames of 256 / 512 B 8 lanes per packet, 5.27 / 7.17 us
+// against the span kernel's 6.16 / 8.75; 256 K / 1 M frames of 768 B the span
+// kernel, 37.2 / 151.6 us against rx_kernel's sorted rounds 41.5 / 167.8
+// (which a 64 / 1500 B mix of 800 B average slots needs: 141.7 against 183.1
+// at 1 M); 1 M frames of 4 KiB the wave kernel, 620.6 against 655.4 us
+// (256 K: rx_kernel 165.7 against 171.4; 9000 B frames stay on rx_kernel).
+constexpr uint64_t kSpanNarrowUpToSlot = 896;
+constexpr uint64_t kWaveNarrowUpToSlot = 4096;
+constexpr uint32_t kWaveNarrowFromPkts = 1u << 20;
+
+// Is the hinted batch of one size class: every slot within 2x of the
+// smallest (a zero length is a NULL / empty entry and costs nothing)?
+bool narrow_batch(const mtcp_gpu_size_hint *h) {
+    if (!h || h->min_len == 0 || h->max_len < h->min_len) return false;
+    const uint32_t lo = ((uint32_t)h->min_len + 63) & ~63u, hi = ((uint32_t)h->max_len + 63) & ~63u;
+    return hi <= 2 * lo;
+}
+
+// rx: the batch is an rx launch (the span kernel exists for rx only);
+// narrow: a hint says the batch is of one size class (narrow_batch)
+int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_only, bool rx,
+               bool narrow = false) {
     int s = ctx->sched;
     if (s == kSchedAuto) {
-        const int big = slot <= kQuadOnlyUpToSlot ? kSchedQuad
-                        : slot <= kSpanUpToSlot   ? kSchedSpan
-                        : (n <= kOctUpToPkts && slot <= kOctUpToSlot) ? kSchedOct : kSchedBig;
-        if (slot < 256) s = n <= 2048 ? kSchedWave : n <= (1u << 17) ? kSchedQuad : big;
-        else if (slot >= 4096) s = n <= (1u << 16) ? kSchedWave : kSchedBig;
-        else s = n <= 8192 ? kSchedWave : n <= (1u << 15) ? kSchedRow : big;
+        int big = slot <= kQuadOnlyUpToSlot ? kSchedQuad
+                  : slot <= kSpanUpToSlot   ? kSchedSpan
+                  : (n <= kOctUpToPkts && slot <= kOctUpToSlot) ? kSchedOct : kSchedBig;
+        if (narrow && slot > kQuadOnlyUpToSlot && slot <= kSpanUpToSlot && n <= kOctUpToPkts)
+            big = kSchedOct;
+        else if (narrow && slot > kSpanUpToSlot && slot <= kSpanNarrowUpToSlot && n > kOctUpToPkts)
+            big = kSchedSpan;
+        if (slot < 256) {
+            s = n <= 2048 ? kSchedWave : n <= (1u << 17) ? kSchedQuad : big;
+        } else if (slot >= 4096) {
+            s = n <= (1u << 16) || (narrow && slot <= kWaveNarrowUpToSlot && n >= kWaveNarrowFromPkts)
+                    ? kSchedWave : kSchedBig;
+        } else {
+            // 16 K frames of 2 KiB slots: the wave kernel, 8.64 against the
+            // row kernel's 9.09 us (1500 B frames keep the rows: 7.28 / 8.27)
+            s = n <= 8192 || (slot >= 2048 && n <= 16384) ? kSchedWave
+                : n <= (1u << 15)                          ? kSchedRow : big;
+        }
     }
     if (s == kSchedSpan && !rx) s = kSchedBig;
     if (s == kSchedBig && small_only) s = kSchedRow;
@@ -329,13 +371,14 @@ uint64_t record_size(const mg::KParams &kp) { return kp.compact ? 16 : 40; }
 uint64_t record_size(const mtcp_gpu_ctx *ctx) { return (ctx->flags & MTCP_GPU_F_COMPACT) ? 16 : 40; }
 
 template <int MODE>
-int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st) {
+int launch(mtcp_gpu_ctx *ctx, const mg::KParams &kp, hipStream_t st, const mtcp_gpu_size_hint *hint = nullptr) {
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     if (kp.n == 0) return MTCP_GPU_OK;
     const bool rss = !mg::is_tx(MODE) && (ctx->flags & MTCP_GPU_F_RSS);
     const bool ptrs = MODE == mg::kRxPtrs || MODE == mg::kTxPtrs;
     const uint64_t avg_slot = ptrs ? 1024 : kp.buf_len / kp.n;
     const int sched = pick_sched(ctx, kp.n, avg_slot, MODE == mg::kTxPtrs || kp.tx_report != nullptr,
-                                 !mg::is_tx(MODE));
+                                 !mg::is_tx(MODE), !ptrs && narrow_batch(hint));
     if (sched != kSchedBig) {
         ctx->last_kernel = rss ? launch_small<MODE, true>(sched, kp.n, avg_slot, st, kp)
                                : launch_small<MODE, false>(sched, kp.n, avg_slot, st, kp);
@@ -390,7 +433,8 @@ hipStream_t pick(mtcp_gpu_ctx *ctx, void *stream) {
     return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
 }
 
-int stage_reserve(Stage &s, uint64_t bytes, uint32_t pkts) {
+int stage_reserve(mtcp_gpu_ctx *ctx, Stage &s, uint64_t bytes, uint32_t pkts) {
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     // a stage's stream exists once a host call uses the stage (a context
     // that only launches device-resident work, or serves an io_module's
     // rxqs, has the one stream of mtcp_gpu_open)
@@ -420,6 +464,16 @@ int stage_reserve(Stage &s, uint64_t bytes, uint32_t pkts) {
         s.pkt_cap = pkts;
     }
     return MTCP_GPU_OK;
+}
+
+// The size hint of a host-side batch: its smallest and largest non-zero
+// frame length ({0, 0} when every length is 0).
+mtcp_gpu_size_hint size_hint(const mtcp_gpu_desc *desc, uint32_t n) {
+    mtcp_gpu_size_hint h = {0xFFFF, 0};
+    for (uint32_t i = 0; i < n; ++i)
+        if (desc[i].len) h.min_len = std::min(h.min_len, desc[i].len), h.max_len = std::max(h.max_len, desc[i].len);
+    if (!h.max_len) h.min_len = 0;
+    return h;
 }
 
 bool offsets_sorted(const mtcp_gpu_desc *desc, uint32_t n) {
@@ -505,6 +559,14 @@ int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rs
 
 void mtcp_gpu_close(mtcp_gpu_ctx *ctx) {
     if (!ctx) return;
+    if (ctx->abandoned) {
+        // work a timed-out call gave up on may still copy into the staging:
+        // leave every stream and buffer allocated (never touched again)
+        // rather than block on a device that stopped answering or free
+        // memory under its DMA; only the host-side struct goes
+        delete ctx;
+        return;
+    }
     DeviceGuard dg(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto &s : ctx->stage) {
@@ -520,6 +582,7 @@ void mtcp_gpu_close(mtcp_gpu_ctx *ctx) {
     if (ctx->h_gather_desc) (void)hipHostFree(ctx->h_gather_desc);
     if (ctx->d_rss_tables) (void)hipFree(ctx->d_rss_tables);
     if (ctx->d_count) (void)hipFree(ctx->d_count);
+    if (ctx->done_evt) (void)hipEventDestroy(ctx->done_evt);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -536,7 +599,7 @@ int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
                        : max_bytes > kStageBytes || max_pkts > kStagePkts ? kStages
                                                                           : 1;
     for (int i = 0; i < stages; ++i) {
-        const int rc = stage_reserve(ctx->stage[i], ((bytes + 15) & ~15ull) + 16, std::max(pkts, 1u));
+        const int rc = stage_reserve(ctx, ctx->stage[i], ((bytes + 15) & ~15ull) + 16, std::max(pkts, 1u));
         if (rc != MTCP_GPU_OK) return rc;
     }
     // a stream sets up its copy queues on its first large copy (7.8 ms
@@ -581,12 +644,23 @@ int mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp) {
 
 void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+void *mtcp_gpu_host_stream(mtcp_gpu_ctx *ctx) {
+    if (!ctx || ctx->abandoned) return nullptr;
+    Stage &s = ctx->stage[0];
+    if (!s.stream) {
+        DeviceGuard dg(ctx->device);
+        if (!dg.ok || !HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking))) return nullptr;
+    }
+    return (void *)s.stream;
+}
+
 uint32_t mtcp_gpu_record_size(const mtcp_gpu_ctx *ctx) { return ctx ? (uint32_t)record_size(ctx) : 0u; }
 
 const char *mtcp_gpu_last_kernel(const mtcp_gpu_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
 
 int mtcp_gpu_sync(mtcp_gpu_ctx *ctx) {
     if (!ctx) return MTCP_GPU_EINVAL;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     DeviceGuard dg(ctx->device);
     return HIP_OK(hipStreamSynchronize(ctx->stream)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
 }
@@ -594,6 +668,13 @@ int mtcp_gpu_sync(mtcp_gpu_ctx *ctx) {
 int mtcp_gpu_rx_chunk_flow_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
                                const mtcp_gpu_desc *d_desc, uint32_t n, uint32_t off_shift,
                                mtcp_gpu_result *d_out, uint32_t *d_bins, void *stream) {
+    return mtcp_gpu_rx_chunk_hint_dev(ctx, d_buf, buf_len, d_desc, n, off_shift, d_out, d_bins, nullptr, stream);
+}
+
+int mtcp_gpu_rx_chunk_hint_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
+                               const mtcp_gpu_desc *d_desc, uint32_t n, uint32_t off_shift,
+                               mtcp_gpu_result *d_out, uint32_t *d_bins, const mtcp_gpu_size_hint *hint,
+                               void *stream) {
     if (!ctx || (n && (!d_buf || !d_desc || !d_out)) || off_shift > 16 || (buf_len & 15) ||
         ((uintptr_t)d_buf & 15) || ((uintptr_t)d_out & out_align(ctx)) || ((uintptr_t)d_desc & 7) ||
         ((uintptr_t)d_bins & 3))
@@ -607,7 +688,7 @@ int mtcp_gpu_rx_chunk_flow_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t bu
     kp.off_shift = off_shift;
     kp.out = d_out;
     kp.bins = d_bins;
-    return launch<mg::kRxChunk>(ctx, kp, pick(ctx, stream));
+    return launch<mg::kRxChunk>(ctx, kp, pick(ctx, stream), hint);
 }
 
 int mtcp_gpu_rx_chunk_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
@@ -679,12 +760,13 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
     if (!offsets_sorted(desc, n)) {
         // arbitrary order: stage the whole chunk once, then batches of descriptors
         Stage &s = ctx->stage[0];
-        rc = stage_reserve(s, ((buf_len + 15) & ~15ull) + 16, kStagePkts);
+        rc = stage_reserve(ctx, s, ((buf_len + 15) & ~15ull) + 16, kStagePkts);
         if (rc == MTCP_GPU_OK &&
             !HIP_OK(hipMemcpyAsync(s.d_buf, buf, buf_len, hipMemcpyHostToDevice, s.stream)))
             rc = MTCP_GPU_EIO;
         for (uint32_t first = 0; first < n && rc == MTCP_GPU_OK; first += kStagePkts) {
             const uint32_t cnt = std::min(n - first, kStagePkts);
+            const mtcp_gpu_size_hint hint = size_hint(desc + first, cnt);
             mg::KParams kp = base_params(ctx);
             kp.buf = s.d_buf;
             kp.buf_len = buf_len;
@@ -695,7 +777,7 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
             if (!HIP_OK(hipMemcpyAsync(s.d_desc, desc + first, (size_t)cnt * sizeof(mtcp_gpu_desc),
                                        hipMemcpyHostToDevice, s.stream)))
                 rc = MTCP_GPU_EIO;
-            if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream);
+            if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream, &hint);
             if (rc == MTCP_GPU_OK &&
                 !HIP_OK(hipMemcpyAsync(out_b + first * rec, s.d_out, cnt * rec,
                                        hipMemcpyDeviceToHost, s.stream)))
@@ -709,16 +791,20 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
                                          buf_len & ~15ull);
             uint64_t hi = lo;
             uint32_t cnt = 0;
+            mtcp_gpu_size_hint hint = {0xFFFF, 0};
             while (first + cnt < n && cnt < kStagePkts) {
                 const uint64_t p = (uint64_t)desc[first + cnt].offset << off_shift;
-                const uint64_t end = std::max(std::min(p + desc[first + cnt].len, buf_len), lo);
+                const uint16_t len = desc[first + cnt].len;
+                const uint64_t end = std::max(std::min(p + len, buf_len), lo);
                 if (cnt > 0 && std::max(hi, end) - lo > kStageBytes) break;
                 hi = std::max(hi, end);
+                if (len) hint.min_len = std::min(hint.min_len, len), hint.max_len = std::max(hint.max_len, len);
                 ++cnt;
             }
+            if (!hint.max_len) hint.min_len = 0;
             Stage &s = ctx->stage[b % kStages];
             const uint64_t span = hi - lo;
-            rc = stage_reserve(s, ((span + 15) & ~15ull) + 16, kStagePkts);
+            rc = stage_reserve(ctx, s, ((span + 15) & ~15ull) + 16, kStagePkts);
             if (rc != MTCP_GPU_OK) break;
             mg::KParams kp = base_params(ctx);
             kp.buf = s.d_buf;
@@ -733,7 +819,7 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
                 !HIP_OK(hipMemcpyAsync(s.d_desc, desc + first, (size_t)cnt * sizeof(mtcp_gpu_desc),
                                        hipMemcpyHostToDevice, s.stream)))
                 rc = MTCP_GPU_EIO;
-            if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream);
+            if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream, &hint);
             if (rc == MTCP_GPU_OK &&
                 !HIP_OK(hipMemcpyAsync(out_b + first * rec, s.d_out, cnt * rec,
                                        hipMemcpyDeviceToHost, s.stream)))
@@ -755,6 +841,7 @@ namespace {
 // aligned slots, pslib.c:146) with its descriptors; *total = chunk bytes.
 int gather_burst(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *lens, uint32_t n,
                  uint64_t *total_out) {
+    if (ctx->abandoned) return MTCP_GPU_EIO;     // its staging may still be under DMA
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) total += ((uint64_t)lens[i] + 63) & ~63ull;
     if (total > ctx->h_gather_cap) {
@@ -806,19 +893,29 @@ int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16
 // tx fill of a host pointer burst (a DPDK wmbufs[].m_table, dpdk_module.c:341-370):
 // the frames are gathered into pinned staging and checked on the GPU, which
 // reports {checks, T} per frame (rx_wave_kernel report mode); only the two
-// check fields are written back into the caller's frames, here on the host.
-int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_t *lens, uint32_t n,
-                          uint32_t *n_filled) {
+// check fields are written back into the caller's frames, here on the host,
+// once the report is in.  With a limit (timeout_us > 0) the wait for the
+// report polls a completion event: past the limit nothing has been written
+// into the caller's frames, the call answers MTCP_GPU_ETIMEDOUT and the
+// context is abandoned (the copies may still run into its staging).  mTCP's
+// own tx fill never waits on a device (tcp_out.c:320-329, ip_out.c:147-165,
+// run from RunMainLoop core.c:818-824): the caller fills the frames itself.
+int mtcp_gpu_tx_fill_ptrs_for(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_t *lens, uint32_t n,
+                              uint32_t *n_filled, uint32_t timeout_us) {
     if (!ctx || (n && (!pkts || !lens))) return MTCP_GPU_EINVAL;
     if (n_filled) *n_filled = 0;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
     uint64_t total = 0;
     int rc = gather_burst(ctx, pkts, lens, n, &total);
     if (rc != MTCP_GPU_OK) return rc;
     Stage &s = ctx->stage[0];
-    rc = stage_reserve(s, ((total + 15) & ~15ull) + 16, n);
+    rc = stage_reserve(ctx, s, ((total + 15) & ~15ull) + 16, n);
     if (rc != MTCP_GPU_OK) return rc;
+    if (timeout_us && !ctx->done_evt &&
+        !HIP_OK(hipEventCreateWithFlags(&ctx->done_evt, hipEventDisableTiming)))
+        return MTCP_GPU_EIO;
     uint2 *report = reinterpret_cast<uint2 *>(ctx->h_gather_desc);    // reused once the H2D is done
     static_assert(sizeof(uint2) == sizeof(mtcp_gpu_desc), "report reuses the descriptor staging");
     if (!HIP_OK(hipMemcpyAsync(s.d_buf, ctx->h_gather, total, hipMemcpyHostToDevice, s.stream)) ||
@@ -836,6 +933,22 @@ int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_
     if (rc == MTCP_GPU_OK && !HIP_OK(hipMemcpyAsync(report, s.d_out, (size_t)n * sizeof(uint2),
                                                     hipMemcpyDeviceToHost, s.stream)))
         rc = MTCP_GPU_EIO;
+    if (timeout_us && rc == MTCP_GPU_OK) {
+        if (!HIP_OK(hipEventRecord(ctx->done_evt, s.stream))) rc = MTCP_GPU_EIO;
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+        while (rc == MTCP_GPU_OK) {
+            const hipError_t e = hipEventQuery(ctx->done_evt);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) {
+                rc = MTCP_GPU_EIO;
+            } else if (std::chrono::steady_clock::now() >= deadline) {
+                ctx->abandoned = true;
+                return MTCP_GPU_ETIMEDOUT;
+            }
+        }
+    }
+    // an enqueue that failed still drains the stream: a queued H2D may be
+    // reading the staging (unbounded, as in every call without a limit)
     if (!HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK) rc = MTCP_GPU_EIO;
     if (rc != MTCP_GPU_OK) return rc;
     uint32_t cnt = 0;
@@ -851,6 +964,11 @@ int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_
     return MTCP_GPU_OK;
 }
 
+int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_t *lens, uint32_t n,
+                          uint32_t *n_filled) {
+    return mtcp_gpu_tx_fill_ptrs_for(ctx, pkts, lens, n, n_filled, 0);
+}
+
 int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mtcp_gpu_desc *desc,
                      uint32_t n, uint32_t off_shift, uint32_t *n_filled) {
     if (!ctx || (n && (!buf || !desc)) || off_shift > 16) return MTCP_GPU_EINVAL;
@@ -859,7 +977,7 @@ int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mt
     DeviceGuard dg(ctx->device);
     Stage &s = ctx->stage[0];
     const uint64_t cap = (buf_len + 15) & ~15ull;
-    int rc = stage_reserve(s, cap + 16, n);
+    int rc = stage_reserve(ctx, s, cap + 16, n);
     if (rc != MTCP_GPU_OK) return rc;
     // an enqueue that fails still drains the stream below: an H2D already
     // queued may be reading the caller's buf
@@ -893,6 +1011,7 @@ int mtcp_gpu_flow_hash_dev(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *d_res, uint
     if (!ctx || (n && (!d_res || !d_bins)) || ((uintptr_t)d_res & 7) || ((uintptr_t)d_bins & 3) ||
         (ctx->flags & MTCP_GPU_F_COMPACT))          // reads 40 B records (the 4-tuple)
         return MTCP_GPU_EINVAL;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
     const uint32_t blocks = std::min<uint32_t>((n + mg::kBlock - 1) / mg::kBlock,
@@ -908,7 +1027,7 @@ int mtcp_gpu_flow_hash(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *res, uint32_t n
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
     Stage &s = ctx->stage[0];
-    int rc = stage_reserve(s, (uint64_t)n * sizeof(uint32_t), n);
+    int rc = stage_reserve(ctx, s, (uint64_t)n * sizeof(uint32_t), n);
     if (rc != MTCP_GPU_OK) return rc;
     uint32_t *d_bins = reinterpret_cast<uint32_t *>(s.d_buf);
     if (!HIP_OK(hipMemcpyAsync(s.d_out, res, (size_t)n * sizeof(mtcp_gpu_result),
@@ -928,6 +1047,7 @@ int mtcp_gpu_rss_queue_map_dev(mtcp_gpu_ctx *ctx, uint32_t saddr_base_h, uint32_
                                int endian_check, uint8_t *d_queue, void *stream) {
     if (!ctx || num_queues < 1 || (num_addr && !d_queue) || ((uintptr_t)d_queue & 3))
         return MTCP_GPU_EINVAL;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     if (num_addr == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
     mg::PoolParams pp{};
@@ -957,6 +1077,7 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues, uint3
     const uint64_t total = (uint64_t)num_addr * mg::kPorts;
     if (total > (uint64_t)INT32_MAX) return MTCP_GPU_EINVAL;
     const uint32_t num_entry = (uint32_t)((int)total / num_queues);
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     if (num_addr == 0 || core < 0 || core >= num_queues) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
     const uint32_t nb = (uint32_t)((total + mg::kPoolTile - 1) / mg::kPoolTile);

@@ -20,7 +20,12 @@
 //                   wave; the last lane of each frame's run in the window
 //                   adds the run's sum (scan minus the scan before the run)
 //                   to the wave's LDS sum of that frame — one lane per frame
-//                   per window, so the adds never collide
+//                   per window, so the adds never collide; the add is an
+//                   LDS atomic only because that is one ds_add_u32 with no
+//                   return (a plain += is a ds_read, a wait and a ds_write).
+//                   Headroom: a 65 535 B frame is 4 097 chunks of at most
+//                   8 x 0xFFFF, 2.15e9 < 2^32 (tests/test_gpu_wave.py
+//                   test_max_length_frames_every_schedule)
 //   headers         chunks 0..6 and the last chunk of every frame go to LDS
 //                   packet-minor, as in rx_kernel, for parse_finish
 // After one barrier wave 0 runs phase 2 with one lane per frame (the code

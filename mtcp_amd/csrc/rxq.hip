@@ -48,6 +48,9 @@ struct mtcp_gpu_rxq {
     uint32_t inflight = 0;               // frames of an unfinished flush_async (0: none)
     bool abandoned = false;              // a flush timed out in rxq_wait_for: no more flushes
     uint64_t used = 0;                   // staging bytes in use
+    // the frames staged since the last flush: smallest and largest non-zero
+    // length, the size hint of their launch (mtcp_gpu_size_hint)
+    uint16_t size_min = 0xFFFF, size_max = 0;
     // A/B knobs (environment at create): MTCP_GPU_STAGE=plain copies frames
     // with memcpy (cached stores) instead of streaming stores;
     // MTCP_GPU_SERVE_AHEAD=k prefetches frame i + k's header and result when
@@ -188,6 +191,10 @@ int mtcp_gpu_rxq_push(mtcp_gpu_rxq *q, const uint8_t *frame, uint16_t len) {
     }
     q->used += slot;
     q->n++;
+    if (len) {
+        q->size_min = len < q->size_min ? len : q->size_min;
+        q->size_max = len > q->size_max ? len : q->size_max;
+    }
     return MTCP_GPU_OK;
 }
 
@@ -220,9 +227,12 @@ int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
     if (hipMemcpyAsync(q->d_buf + lo, q->buf + lo, q->used - lo + dbytes, hipMemcpyHostToDevice,
                        q->stream) != hipSuccess)
         return MTCP_GPU_EIO;
-    int rc = mtcp_gpu_rx_chunk_dev(q->ctx, q->d_buf, q->used,
-                                   reinterpret_cast<const mtcp_gpu_desc *>(q->d_buf + q->used), cnt,
-                                   6, reinterpret_cast<mtcp_gpu_result *>(q->d_out), q->stream);
+    // every length was seen at push: the launch gets the batch's size class
+    const mtcp_gpu_size_hint hint = {q->size_max ? q->size_min : (uint16_t)0, q->size_max};
+    int rc = mtcp_gpu_rx_chunk_hint_dev(q->ctx, q->d_buf, q->used,
+                                        reinterpret_cast<const mtcp_gpu_desc *>(q->d_buf + q->used), cnt,
+                                        6, reinterpret_cast<mtcp_gpu_result *>(q->d_out), nullptr, &hint,
+                                        q->stream);
     if (rc == MTCP_GPU_OK &&
         (hipMemcpyAsync(q->res + (size_t)first * q->rec, q->d_out, (size_t)cnt * q->rec,
                         hipMemcpyDeviceToHost, q->stream) != hipSuccess ||
@@ -233,6 +243,8 @@ int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
         return rc;
     }
     q->inflight = cnt;
+    q->size_min = 0xFFFF;
+    q->size_max = 0;
     return MTCP_GPU_OK;
 }
 
@@ -344,6 +356,8 @@ void mtcp_gpu_rxq_reset(mtcp_gpu_rxq *q) {
     if (!q || q->inflight) return;                 // a flush_async is reading the staging
     q->n = q->done_n = 0;
     q->used = 0;
+    q->size_min = 0xFFFF;
+    q->size_max = 0;
 }
 
 }  // extern "C"

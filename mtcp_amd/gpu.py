@@ -134,11 +134,19 @@ class Context:
         yield None
         torch.cuda.ExternalStream(lib().mtcp_gpu_stream(self._h), device=self.device).synchronize()
 
-    def rx_chunk_dev(self, buf, desc, n: int, off_shift: int, out, stream=None) -> None:
+    def rx_chunk_dev(self, buf, desc, n: int, off_shift: int, out, stream=None, hint=None) -> None:
+        """hint: (min_len, max_len) of the batch's frames -> mtcp_gpu_rx_chunk_hint_dev."""
         with self._ordered(stream) as st:
-            check(lib().mtcp_gpu_rx_chunk_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
-                                              _dptr(desc), n, off_shift, _dptr(out),
-                                              st), "mtcp_gpu_rx_chunk_dev")
+            if hint is None:
+                check(lib().mtcp_gpu_rx_chunk_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
+                                                  _dptr(desc), n, off_shift, _dptr(out),
+                                                  st), "mtcp_gpu_rx_chunk_dev")
+            else:
+                h = (ctypes.c_uint16 * 2)(*hint)
+                check(lib().mtcp_gpu_rx_chunk_hint_dev(self._h, _dptr(buf), buf.numel() * buf.element_size(),
+                                                       _dptr(desc), n, off_shift, _dptr(out), None,
+                                                       ctypes.cast(h, ctypes.c_void_p), st),
+                      "mtcp_gpu_rx_chunk_hint_dev")
 
     def rx_ptrs_dev(self, ptrs, lens, n: int, out, stream=None) -> None:
         with self._ordered(stream) as st:
@@ -197,17 +205,24 @@ class Context:
                                      len(desc), off_shift, ctypes.byref(cnt)), "mtcp_gpu_tx_fill")
         return cnt.value
 
-    def tx_fill_ptrs(self, buf: np.ndarray, offsets, lens) -> int:
+    def tx_fill_ptrs(self, buf: np.ndarray, offsets, lens, timeout_us: int | None = None) -> int:
         """mtcp_gpu_tx_fill_ptrs over frames of the host array `buf` at byte
         `offsets` (a DPDK-style pointer burst into one host buffer); fills
-        `buf` in place and returns the number of frames filled."""
+        `buf` in place and returns the number of frames filled.  With
+        timeout_us: mtcp_gpu_tx_fill_ptrs_for (MtcpGpuError ETIMEDOUT past
+        the limit, the context abandoned)."""
         offsets = np.asarray(offsets, dtype=np.int64)
         n = len(offsets)
         ptrs = (ctypes.c_void_p * max(n, 1))(*[buf.ctypes.data + int(o) for o in offsets])
         lens = np.ascontiguousarray(lens, dtype=np.uint16)
         cnt = ctypes.c_uint32(0)
-        check(lib().mtcp_gpu_tx_fill_ptrs(self._h, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data,
-                                          n, ctypes.byref(cnt)), "mtcp_gpu_tx_fill_ptrs")
+        if timeout_us is None:
+            check(lib().mtcp_gpu_tx_fill_ptrs(self._h, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data,
+                                              n, ctypes.byref(cnt)), "mtcp_gpu_tx_fill_ptrs")
+        else:
+            check(lib().mtcp_gpu_tx_fill_ptrs_for(self._h, ctypes.cast(ptrs, ctypes.c_void_p),
+                                                  lens.ctypes.data, n, ctypes.byref(cnt), timeout_us),
+                  "mtcp_gpu_tx_fill_ptrs_for")
         return cnt.value
 
     # -- flow-table hash (HashFlow, mtcp/src/tcp_stream.c:56-90) -------------

@@ -38,11 +38,10 @@
  * dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers 0 while the GPU path
  * of that interface is healthy and -1 otherwise, so mTCP falls back to its
  * own checksums exactly as with a NIC that lacks the offload
- * (dpdk_dev_ioctl, dpdk_module.c:809-816).  On the receive side every wait
- * on the GPU is bounded (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000, 0: none;
+ * (dpdk_dev_ioctl, dpdk_module.c:809-816).  Every wait on the GPU, receive
+ * and transmit, is bounded (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000, 0: none;
  * clamped to 4294967): a GPU that stops answering is abandoned, never waited
- * on again, and mTCP checks every frame from then on.  (The opt-in transmit
- * fill below is synchronous and not bounded.)
+ * on again, and mTCP checks and fills every frame from then on.
  * NETSTAT: a frame dropped here never reaches ProcessPacket, so get_rptr
  * counts it in rx_packets / rx_bytes as ProcessPacket would have
  * (eth_in.c:20-23) and core.c:774-775 counts the NULL in rx_errors: the three
@@ -55,9 +54,13 @@
  * it hands out, and send_pkts fills the recorded frames' checksums on the
  * GPU (mtcp_gpu_tx_fill_ptrs: only the two check fields are written) before
  * the wrapped backend sends them.  ICMP's IP checksum (PKT_TX_IP_CSUM) stays
- * with mTCP.  If the GPU fails at send time, the recorded frames are filled
- * with mTCP's own ip_fast_csum / TCPCalcChecksum and every later answer is
- * -1.  Off by default: send_pkts is synchronous and mTCP calls it every loop
+ * with mTCP.  The fill waits at most MTCP_GPU_WAIT_TIMEOUT_MS
+ * (mtcp_gpu_tx_fill_ptrs_for), as mTCP's own fill never waits on a device
+ * (tcp_out.c:320-329, ip_out.c:147-165, core.c:818-824).  If the GPU fails
+ * or does not answer in time at send time (or at destroy_handle's last
+ * flush), the recorded frames are filled with mTCP's own ip_fast_csum /
+ * TCPCalcChecksum, the GPU is abandoned and every later answer is -1.
+ * Off by default: send_pkts is synchronous and mTCP calls it every loop
  * with at most a burst (64 frames on DPDK, MAX_PKT_BURST), so each send pays
  * a GPU round trip (gather, H2D, kernel, D2H) that costs more than the CPU's
  * own fill of 64 frames (measured: DESIGN.md §7).
@@ -75,7 +78,7 @@
  * another limit, MTCP_GPU_THREADS=all admits every thread.
  *
  * Fault injection (MTCP_GPU_FAIL_AFTER, MTCP_GPU_STALL_AFTER /
- * MTCP_GPU_STALL_US) exists only in test builds (-DMTCP_GPU_TESTING, linked
+ * MTCP_GPU_TX_STALL_AFTER / MTCP_GPU_STALL_US) exists only in test builds (-DMTCP_GPU_TESTING, linked
  * with tests/c/libmtcp_gpu_testing.so); a production build ignores those
  * variables.
  *
@@ -153,12 +156,14 @@ struct gpu_private_context {
 #ifdef MTCP_GPU_TESTING
     long fail_after;                      /* MTCP_GPU_FAIL_AFTER: fault injection, -1 off */
     long stall_after;                     /* MTCP_GPU_STALL_AFTER: fault injection, -1 off */
+    long tx_stall_after;                  /* MTCP_GPU_TX_STALL_AFTER: fault injection, -1 off */
     uint32_t stall_us;                    /* MTCP_GPU_STALL_US                */
 #endif
     uint32_t wait_us;                     /* MTCP_GPU_WAIT_TIMEOUT_MS, 0: no limit */
     int slot_dev;                         /* device whose admission slot this thread holds, -1 */
     mtcp_gpu_ctx *hung;                   /* abandoned after a timed-out wait: never waited on */
     long launches;                        /* aggregates sent to the GPU       */
+    long tx_fills;                        /* tx flushes sent to the GPU       */
     struct gpu_ifq *ifq[MAX_DEVICES];     /* created at init (or first recv_pkts) */
     int ifq_failed[MAX_DEVICES];          /* no staging: this interface passes through */
     struct gpu_txq *txq[MAX_DEVICES];
@@ -366,6 +371,9 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
      * exercised on a healthy GPU */
     g->stall_after = getenv("MTCP_GPU_STALL_AFTER") ? atol(getenv("MTCP_GPU_STALL_AFTER")) : -1;
     g->stall_us = getenv("MTCP_GPU_STALL_US") ? (uint32_t)atol(getenv("MTCP_GPU_STALL_US")) : 0;
+    /* MTCP_GPU_TX_STALL_AFTER=k: the (k+1)-th tx fill waits MTCP_GPU_STALL_US
+     * behind mtcp_gpu_debug_stall_host (the bounded send_pkts) */
+    g->tx_stall_after = getenv("MTCP_GPU_TX_STALL_AFTER") ? atol(getenv("MTCP_GPU_TX_STALL_AFTER")) : -1;
 #endif
     g->wait_us = gpu_wait_us();
     if (g->tx && !gpu_tx_capable(gpu_inner_module)) {
@@ -376,6 +384,12 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
     ndev = mtcp_gpu_device_count();
     dev = ndev > 0 ? gpu_pick_device(ctx->cpu, ndev) : -1;
     if (dev >= 0 && !gpu_thread_admit(dev)) {
+        /* said once per refused thread, at init: a deployment with more
+         * threads than the limit per GPU sees where its offload went */
+        TRACE_CONFIG("gpu_module: core %d: GPU %d already serves %d mTCP threads "
+                     "(MTCP_GPU_THREADS, default %d); this thread checks its own frames "
+                     "(MTCP_GPU_THREADS=all offloads every thread)\n",
+                     ctx->cpu, dev, gpu_thread_limit(), GPU_THREADS_DEFAULT);
         g->passthrough = 1;                  /* mTCP's own checksums on this core */
         return;
     }
@@ -437,17 +451,30 @@ static void gpu_tx_fill_sw(uint8_t *pkt, uint16_t len)
                                   iph->saddr, iph->daddr);
 }
 
-/* Fill the checksums of the frames recorded for interface nif. */
+/* Fill the checksums of the frames recorded for interface nif: on the GPU,
+ * waiting at most MTCP_GPU_WAIT_TIMEOUT_MS; a GPU that does not report in
+ * time is abandoned (nothing of it was written into the frames) and the
+ * frames are filled here, as after any other GPU error. */
 static void gpu_tx_flush(struct gpu_private_context *g, int nif)
 {
     struct gpu_txq *t = g->txq[nif];
     uint32_t i;
+    int rc;
 
     if (!t || !t->n)
         return;
-    if (g->gpu &&
-        mtcp_gpu_tx_fill_ptrs(g->gpu, t->pkt, t->len, t->n, NULL) != MTCP_GPU_OK)
-        gpu_fail(g);
+    if (g->gpu) {
+#ifdef MTCP_GPU_TESTING
+        if (g->tx_fills == g->tx_stall_after)
+            (void)mtcp_gpu_debug_stall_host(g->gpu, g->stall_us);
+#endif
+        g->tx_fills++;
+        rc = mtcp_gpu_tx_fill_ptrs_for(g->gpu, t->pkt, t->len, t->n, NULL, g->wait_us);
+        if (rc == MTCP_GPU_ETIMEDOUT)
+            gpu_abandon(g);                   /* never waited on (or closed) again */
+        else if (rc != MTCP_GPU_OK)
+            gpu_fail(g);
+    }
     if (!g->gpu)                              /* mTCP skipped these: fill them here */
         for (i = 0; i < t->n; i++)
             gpu_tx_fill_sw(t->pkt[i], t->len[i]);
@@ -474,6 +501,8 @@ static uint8_t *gpu_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uint16_
     }
     if (t->n == GPU_TX_MAX)
         gpu_tx_flush(g, ifidx);
+    if (!g->gpu)
+        return p;     /* abandoned: dev_ioctl answers -1, mTCP fills this frame itself */
     t->pkt[t->n] = p;
     t->len[t->n] = len;
     t->n++;

@@ -41,6 +41,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "mtcp.h"
 #include "io_module.h"
@@ -65,12 +66,16 @@ uint16_t __wrap_TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uin
 }
 
 static int g_ioctl_peek = -2, g_ioctl_tcpip = -2, g_ioctl_ip = -2;
+static uint32_t g_tcpip_zero, g_tcpip_sw;     /* PKT_TX_TCPIP_CSUM answers 0 / -1 */
 static io_module_func g_observed;
 static int32_t observe_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp)
 {
     int32_t r = gpu_module_func.dev_ioctl(ctx, nif, cmd, argp);
     if (cmd == PKT_TX_TCPIP_CSUM_PEEK) g_ioctl_peek = r;
-    if (cmd == PKT_TX_TCPIP_CSUM) g_ioctl_tcpip = r;
+    if (cmd == PKT_TX_TCPIP_CSUM) {
+        g_ioctl_tcpip = r;
+        if (r == 0) g_tcpip_zero++; else g_tcpip_sw++;
+    }
     if (cmd == PKT_TX_IP_CSUM) g_ioctl_ip = r;
     return r;
 }
@@ -139,6 +144,24 @@ static io_module_func nic_module = {
     .get_rptr = nic_rptr, .recv_pkts = nic_recv, .select = nic_select,
     .destroy_handle = nic_destroy, .dev_ioctl = NULL,
 };
+
+/* the longest send_pkts (RunMainLoop's tx section, core.c:818-824, must not
+ * block on a device) and the destroy_handle time, in seconds */
+static double g_max_send_s, g_destroy_s;
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+static void send_timed(mtcp_manager_t mtcp, struct mtcp_thread_context *ctx)
+{
+    double t0 = now_s(), dt;
+    mtcp->iom->send_pkts(ctx, 0);
+    dt = now_s() - t0;
+    if (dt > g_max_send_s)
+        g_max_send_s = dt;
+}
 
 static uint64_t g_rng = 0x2545F4914F6CDD1Dull;
 static uint64_t rnd(void)
@@ -220,7 +243,7 @@ int main(int argc, char **argv)
         if (i % 97 == 96) {
             /* an ICMP datagram: IP checksum per PKT_TX_IP_CSUM (ip_out.c:86-88) */
             uint8_t *p = IPOutputStandalone(mtcp, IPPROTO_ICMP, (uint16_t)i, saddr, daddr, 64);
-            if (!p) { refused++; mtcp->iom->send_pkts(&ctx, 0); continue; }
+            if (!p) { refused++; send_timed(mtcp, &ctx); continue; }
             for (k = 0; k < 64; k++) p[k] = (uint8_t)rnd();
             icmp_frames++;
         } else {
@@ -235,25 +258,31 @@ int main(int argc, char **argv)
                                         (uint32_t)rnd(), (uint16_t)rnd(), flags, payload,
                                         (uint16_t)len, (uint32_t)rnd(), (uint32_t)rnd()) < 0) {
                 refused++;
-                mtcp->iom->send_pkts(&ctx, 0);
+                send_timed(mtcp, &ctx);
                 continue;
             }
             tcp_frames++;
         }
         if ((i + 1) % BURST == 0)
-            mtcp->iom->send_pkts(&ctx, 0);               /* core.c:818-824 */
+            send_timed(mtcp, &ctx);                      /* core.c:818-824 */
     }
-    mtcp->iom->send_pkts(&ctx, 0);
-    mtcp->iom->destroy_handle(&ctx);
+    send_timed(mtcp, &ctx);
+    {
+        double t0 = now_s();
+        mtcp->iom->destroy_handle(&ctx);
+        g_destroy_s = now_s() - t0;
+    }
 
     out = fopen(argv[1], "wb");
     if (!out || fwrite(g_nic->out, SLOT, g_nic->sent, out) != g_nic->sent) { perror(argv[1]); return 1; }
     fclose(out);
     printf("{\"frames\": %u, \"sent\": %u, \"tcp\": %u, \"icmp\": %u, \"refused\": %u, "
            "\"send_calls\": %d, \"tcp_csum_calls\": %llu, \"ioctl_peek\": %d, \"ioctl_tcpip\": %d, "
-           "\"ioctl_ip\": %d, \"observe\": %d}\n",
+           "\"ioctl_ip\": %d, \"observe\": %d, \"max_send_s\": %.6f, \"destroy_s\": %.6f, "
+           "\"tcpip_zero\": %u, \"tcpip_sw\": %u}\n",
            n, g_nic->sent, tcp_frames, icmp_frames, refused, g_nic->send_calls,
-           (unsigned long long)g_tcp_csum_calls, g_ioctl_peek, g_ioctl_tcpip, g_ioctl_ip, observe);
+           (unsigned long long)g_tcp_csum_calls, g_ioctl_peek, g_ioctl_tcpip, g_ioctl_ip, observe,
+           g_max_send_s, g_destroy_s, g_tcpip_zero, g_tcpip_sw);
     free(g_nic->out);
     free(g_nic);
     free(mtcp);

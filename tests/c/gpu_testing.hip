@@ -1,6 +1,6 @@
 // gpu_testing.hip — TEST-ONLY library (tests/c/libmtcp_gpu_testing.so): the
 // fault injection the hang tests use (tests/c/mtcp_gpu_testing.h), built on
-// the product's public ABI only (mtcp_gpu_stream), so that the product
+// the product's public ABI only (mtcp_gpu_stream, mtcp_gpu_host_stream), so that the product
 // library exports no debug entry point.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,9 +17,9 @@ __global__ __launch_bounds__(64) void stall_kernel(uint64_t ticks) {
 }
 }  // namespace
 
-extern "C" int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us) {
-    if (!ctx || us > 10u * 1000 * 1000) return MTCP_GPU_EINVAL;
-    hipStream_t st = reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx));
+namespace {
+int stall_on(hipStream_t st, uint32_t us) {
+    if (!st || us > 10u * 1000 * 1000) return MTCP_GPU_EINVAL;
     hipDevice_t dev = 0;
     int prev = -1;
     if (hipStreamGetDevice(st, &dev) != hipSuccess || hipGetDevice(&prev) != hipSuccess) return MTCP_GPU_ENODEV;
@@ -28,4 +28,15 @@ extern "C" int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us) {
     const bool ok = hipGetLastError() == hipSuccess;
     if (prev != dev) (void)hipSetDevice(prev);
     return ok ? MTCP_GPU_OK : MTCP_GPU_EIO;
+}
+}  // namespace
+
+extern "C" int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us) {
+    if (!ctx) return MTCP_GPU_EINVAL;
+    return stall_on(reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx)), us);
+}
+
+extern "C" int mtcp_gpu_debug_stall_host(mtcp_gpu_ctx *ctx, uint32_t us) {
+    if (!ctx) return MTCP_GPU_EINVAL;
+    return stall_on(reinterpret_cast<hipStream_t>(mtcp_gpu_host_stream(ctx)), us);
 }

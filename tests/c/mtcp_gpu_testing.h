@@ -21,6 +21,11 @@ extern "C" {
  * much later.  MTCP_GPU_EINVAL for a NULL context or a longer stall. */
 int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us);
 
+/* The same on the stream of the context's host-memory calls
+ * (mtcp_gpu_host_stream): the next mtcp_gpu_tx_fill_ptrs[_for] completes
+ * `us` later (the bounded tx fill of gpu_module.c is tested with it). */
+int mtcp_gpu_debug_stall_host(mtcp_gpu_ctx *ctx, uint32_t us);
+
 #ifdef __cplusplus
 }
 #endif

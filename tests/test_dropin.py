@@ -208,12 +208,14 @@ EXE_TX = os.path.join(ROOT, "oracle", "_ref", "dropin_tx")
 TX_SLOT = 2048
 
 
-def run_dropin_tx(tmp_path, n=4096, tx="1", mode="observe"):
+def run_dropin_tx(tmp_path, n=4096, tx="1", mode="observe", inject=None):
     if not os.path.exists(EXE_TX):
         pytest.fail("oracle/_ref/dropin_tx not built: `make -C oracle ref` (needs /root/reference)")
-    out = tmp_path / f"tx_{tx}_{mode}.bin"
+    out = tmp_path / f"tx_{tx}_{mode}_{bool(inject)}.bin"
+    env = dict(os.environ, MTCP_GPU_TX=tx, MTCP_GPU_PIPELINE="1")
+    env.update(inject or {})
     p = subprocess.run([EXE_TX, str(out), str(n), mode], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, MTCP_GPU_TX=tx, MTCP_GPU_PIPELINE="1"))
+                       env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     stats = json.loads(p.stdout.strip().splitlines()[-1])
     recs = np.fromfile(out, dtype=np.uint8).reshape(-1, TX_SLOT)
@@ -266,6 +268,39 @@ def test_dropin_tx_at_the_reference_call_sites(tmp_path, mode):
         assert stats["ioctl_peek"] == 0 and stats["ioctl_tcpip"] == 0 and stats["ioctl_ip"] == -1
         assert sw_stats["ioctl_peek"] == -1 and sw_stats["ioctl_tcpip"] == -1
     assert stats["send_calls"] >= len(recs) // 64
+    assert np.array_equal(recs, sw)
+    v, proto = tx_frames_verify(recs)
+    assert (v[proto == 6] == 0).all() and (v[proto == 1] == 6).all()
+
+
+@pytest.mark.gpu
+def test_dropin_tx_gpu_hang_falls_back_to_mtcp(tmp_path):
+    """The tx fill never blocks mTCP's main loop on a GPU that stops
+    answering (mTCP's own fill never waits on a device: tcp_out.c:320-329,
+    ip_out.c:147-165, run from core.c:818-824).  The third send_pkts' fill
+    waits 1.5 s on the GPU behind mtcp_gpu_debug_stall_host; gpu_module's
+    wait gives up after MTCP_GPU_WAIT_TIMEOUT_MS (100 ms), fills those frames
+    with mTCP's ip_fast_csum / TCPCalcChecksum, abandons the GPU, and answers
+    dev_ioctl -1 from then on, so mTCP fills the rest itself.  Every
+    send_pkts and the shutdown return within the limit (plus the software
+    fill), far below the stall, and the frames sent equal, byte for byte,
+    those the reference fills itself (MTCP_GPU_TX=0)."""
+    inject = {"MTCP_GPU_TX_STALL_AFTER": "2", "MTCP_GPU_STALL_US": "1500000",
+              "MTCP_GPU_WAIT_TIMEOUT_MS": "100"}
+    stats, recs = run_dropin_tx(tmp_path, tx="1", mode="observe", inject=inject)
+    sw_stats, sw = run_dropin_tx(tmp_path, tx="0", mode="observe")
+    assert stats["sent"] == stats["frames"] == sw_stats["sent"] == len(recs) and stats["refused"] == 0
+    # the GPU filled the first bursts' frames (dev_ioctl 0), mTCP the frames
+    # built after the timed-out fill (dev_ioctl -1)
+    assert stats["tcpip_zero"] >= 128 and stats["tcpip_sw"] > 3000
+    assert stats["tcpip_zero"] + stats["tcpip_sw"] == stats["tcp"]
+    # TCPCalcChecksum ran for mTCP's own fills plus gpu_module's fill of the
+    # one burst whose GPU fill timed out (at most 64 frames), no frame twice
+    assert 0 < stats["tcp_csum_calls"] - stats["tcpip_sw"] <= 64
+    assert stats["ioctl_tcpip"] == -1 and stats["ioctl_peek"] == -1
+    # bounded: no send_pkts and no shutdown waited for the 1.5 s stall
+    assert stats["max_send_s"] < 0.75, stats
+    assert stats["destroy_s"] < 0.75, stats
     assert np.array_equal(recs, sw)
     v, proto = tx_frames_verify(recs)
     assert (v[proto == 6] == 0).all() and (v[proto == 1] == 6).all()

@@ -38,12 +38,12 @@ def dev_results(n):
     return torch.zeros(n * 40, dtype=torch.uint8, device=DEV)
 
 
-def run_rx_dev(ctx, buf: np.ndarray, desc: np.ndarray, off_shift: int):
+def run_rx_dev(ctx, buf: np.ndarray, desc: np.ndarray, off_shift: int, hint=None):
     pad = (-buf.nbytes) % 16
     b = to_dev(np.concatenate([buf, np.zeros(pad, np.uint8)]) if pad else buf)
     d = to_dev(desc)
     out = dev_results(len(desc))
-    ctx.rx_chunk_dev(b, d, len(desc), off_shift, out)
+    ctx.rx_chunk_dev(b, d, len(desc), off_shift, out, hint=hint)
     torch.cuda.synchronize()
     return out.cpu().numpy().view(RESULT_DTYPE)
 

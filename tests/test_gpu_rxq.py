@@ -17,16 +17,17 @@ from mtcp_amd import RESULT_DTYPE
 torch = pytest.importorskip("torch")
 
 V_IP_CSUM_BAD, V_TCP_CSUM_BAD, V_TRUNCATED, V_BAD_DESC = 4, 9, 10, 11
-EINVAL = -22
+EINVAL, ETIMEDOUT, EIO = -22, -110, -5
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def testing_lib():
-    """tests/c/libmtcp_gpu_testing.so: mtcp_gpu_debug_stall, the fault
+def _testing_lib():
+    """tests/c/libmtcp_gpu_testing.so: mtcp_gpu_debug_stall[_host], the fault
     injection the product library does not export (built by build())."""
     T = ctypes.CDLL(os.path.join(ROOT, "tests", "c", "libmtcp_gpu_testing.so"))
-    T.mtcp_gpu_debug_stall.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-    T.mtcp_gpu_debug_stall.restype = ctypes.c_int
+    for f in (T.mtcp_gpu_debug_stall, T.mtcp_gpu_debug_stall_host):
+        f.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        f.restype = ctypes.c_int
     return T
 
 
@@ -94,8 +95,7 @@ def test_rxq_wait_for_abandons_a_flush_that_does_not_finish(golden):
     import time
     from mtcp_amd import gpu
     from mtcp_amd._lib import lib
-    L, T = lib(), testing_lib()
-    ETIMEDOUT, EIO = -110, -5
+    L, T = lib(), _testing_lib()
     buf, desc = golden.buf, golden.desc
     base = buf.ctypes.data
     part = desc[:256]
@@ -149,7 +149,7 @@ def test_rxq_destroy_right_after_a_timeout(golden, stall_ms, leaks):
     import time
     from mtcp_amd import gpu
     from mtcp_amd._lib import lib
-    L, T = lib(), testing_lib()
+    L, T = lib(), _testing_lib()
     buf, desc = golden.buf, golden.desc
     base = buf.ctypes.data
     with gpu.Context(0) as ctx:
@@ -163,11 +163,19 @@ def test_rxq_destroy_right_after_a_timeout(golden, stall_ms, leaks):
         t0 = time.monotonic()
         L.mtcp_gpu_rxq_destroy(q)
         dt = time.monotonic() - t0
-        if leaks:
-            assert 0.09 <= dt < 0.3, dt
-        else:
-            assert dt < 0.1, dt
+        # what destroy did, read from the stream rather than from its own
+        # duration: when it freed the buffers it had waited for the flush, so
+        # the stream is idle and the sync returns at once; when it leaked them
+        # it returned after its 100 ms bound with the stall still running
+        t1 = time.monotonic()
         assert L.mtcp_gpu_sync(ctx._h) == 0
+        sync_dt = time.monotonic() - t1
+        if leaks:
+            assert 0.09 <= dt < 0.3, dt                  # bounded: not the 400 ms stall
+            assert sync_dt > 0.05, sync_dt               # the flush was still running
+        else:
+            assert dt < 0.1 + 0.2, dt                    # never past its bound (+ load margin)
+            assert sync_dt < 0.05, sync_dt               # it waited for the flush, then freed
         # the context still works: a fresh rxq checks frames
         q = ctypes.c_void_p()
         assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 64, 64 * 2048) == 0
@@ -178,3 +186,46 @@ def test_rxq_destroy_right_after_a_timeout(golden, stall_ms, leaks):
             assert L.mtcp_gpu_rxq_flush(q, ctypes.byref(n)) == 0 and n.value == 64
         finally:
             L.mtcp_gpu_rxq_destroy(q)
+
+
+@pytest.mark.gpu
+def test_tx_fill_ptrs_for_gives_up_and_abandons(golden):
+    """mtcp_gpu_tx_fill_ptrs_for (gpu_module.c's send_pkts): a fill whose
+    report is not in within the limit answers MTCP_GPU_ETIMEDOUT in about
+    the limit, leaves the caller's frames untouched (nothing is written
+    before the report), and abandons the context: every later call answers
+    EIO without touching the device, and closing it does not wait for the
+    stalled work.  A fresh context fills the same frames as the reference."""
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    import time
+    from mtcp_amd import gpu
+    from mtcp_amd._lib import MtcpGpuError, lib
+    L, T = lib(), _testing_lib()
+    part = golden.desc[:64]
+    offs = part["offset"].astype(np.int64)
+    want = golden.buf.copy()
+    oracle.tx_fill(want, part, 0)
+    ctx = gpu.Context(0)
+    host = golden.buf.copy()
+    assert ctx.tx_fill_ptrs(host, offs, part["len"], timeout_us=2_000_000) > 0   # a healthy fill
+    assert np.array_equal(host, want)
+    host = golden.buf.copy()
+    assert T.mtcp_gpu_debug_stall_host(ctx._h, 800 * 1000) == 0
+    t0 = time.monotonic()
+    with pytest.raises(MtcpGpuError) as e:
+        ctx.tx_fill_ptrs(host, offs, part["len"], timeout_us=30_000)
+    assert e.value.code == ETIMEDOUT
+    assert time.monotonic() - t0 < 0.3
+    assert np.array_equal(host, golden.buf)                  # nothing written
+    with pytest.raises(MtcpGpuError) as e:                   # abandoned: EIO, no device call
+        ctx.tx_fill_ptrs(host, offs, part["len"], timeout_us=30_000)
+    assert e.value.code == EIO
+    assert L.mtcp_gpu_sync(ctx._h) == EIO
+    assert L.mtcp_gpu_host_stream(ctx._h) is None
+    t0 = time.monotonic()
+    ctx.close()
+    assert time.monotonic() - t0 < 0.3                       # not the 800 ms stall
+    with gpu.Context(0) as fresh:
+        assert fresh.tx_fill_ptrs(host, offs, part["len"], timeout_us=2_000_000) > 0
+        assert np.array_equal(host, want)

@@ -148,3 +148,53 @@ def test_bench_default_n2_runs_c4_with_cpu_baseline(gpu, tmp_path):
     assert cb["cores"] == sum(r["cores"] for r in cb["per_rank"])
     # the two ranks share device 0's node: disjoint halves of its cores
     assert line["host_cpus"]["shared_with_ranks"] == [0, 1]
+
+
+def _bench_line(cmd, env, timeout=300):
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _clean_env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MASTER_ADDR="127.0.0.1", **kw)
+    return env
+
+
+def test_bench_default_n1_carries_c4_per_gpu(gpu):
+    """the N = 1 default line (C2) also times C4's
+    per-GPU step — rank 0's 2 M x 1500 B shard, two launches — in the same
+    run, so the driver's 1 -> 8 ratio can be read on identical per-GPU work."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+           "--cpu-baseline", "off", "--pcie", "off", "--small-batch", "off", "--ceiling", "off"]
+    line = _bench_line(cmd, _clean_env())
+    assert line["n_gpus"] == 1 and line["config"]["workload"].startswith("c2: 1 M x 1500 B")
+    c4 = line["c4_per_gpu"]
+    assert "error" not in c4, c4
+    assert c4["packets"] == 1 << 21 and c4["launches_per_step"] == 2 and c4["value"] > 0
+    assert c4["tcp_ok_fraction"] > 0.99
+    assert line["run"]["wall_s_max_rank"] > 0 and line["run"]["host_rss_gb_max_rank"] > 0
+
+
+def test_bench_driver_form_eight_ranks_on_one_device(gpu):
+    """the driver's exact `python3 bench.py --gpus 8`
+    form, rehearsed with all eight ranks on device 0 (MTCP_BENCH_DEVICE=0)
+    at a reduced per-GPU count, every leg on: one JSON line, C4's workload
+    over 8 ranks, the CPU baseline of every rank on its own disjoint core
+    share at once, the PCIe-inclusive leg of all 8 ranks, the run's wall time
+    and host memory.  (The timings mean nothing: 8 ranks share one GPU.)"""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--per-gpu", str(1 << 14),
+           "--steps", "3", "--warmup", "1", "--cpu-sample", str(1 << 13)]
+    line = _bench_line(cmd, _clean_env(MTCP_BENCH_DEVICE="0"))
+    assert line["n_gpus"] == 8 and line["config"]["workload"].startswith("c4: 128 K x 1500 B")
+    assert line["config"]["packets_total"] == 8 << 14 and line["scaling"] == "weak"
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and [r["rank"] for r in cb["per_rank"]] == list(range(8))
+    assert cb["cores"] == sum(r["cores"] for r in cb["per_rank"])
+    assert line["host_cpus"]["shared_with_ranks"] == list(range(8))
+    assert line["pcie_inclusive"]["n_gpus"] == 8 and line["pcie_inclusive"]["value"] > 0
+    assert "c4_per_gpu" not in line
+    assert line["run"]["wall_s_max_rank"] > 0

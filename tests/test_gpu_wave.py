@@ -117,26 +117,39 @@ def imix_lengths(n, seed):
     (32769, 512, "rx_span_kernel"), (32769, 640, "rx_span_kernel"), (32769, 704, "rx_group_kernel<oct"),
     (65536, 1500, "rx_group_kernel<oct"), (65537, 1500, "rx_kernel"), (65536, 4096, "rx_wave"),
     (65537, 4096, "rx_kernel"), (16384, 4032, "rx_group_kernel<row"),
-    ((1 << 18) + 3, "imix", "rx_span_kernel")])
+    ((1 << 18) + 3, "imix", "rx_span_kernel"), (16384, 2048, "rx_wave"), (16385, 2048, "rx_group_kernel<row"),
+    # with the caller's size hint (mtcp_gpu_rx_chunk_hint_dev): one size class
+    ((1 << 16), "256h", "rx_group_kernel<oct"), ((1 << 16) + 1, "256h", "rx_span_kernel"),
+    ((1 << 16), "512h", "rx_group_kernel<oct"), ((1 << 16), 512, "rx_span_kernel"),
+    ((1 << 16) + 1, "768h", "rx_span_kernel"), ((1 << 16) + 1, 768, "rx_kernel"),
+    ((1 << 16) + 1, "1024h", "rx_kernel"), ((1 << 17) + 1, "bimodalh", "rx_kernel<sorted>"),
+    ((1 << 17) + 1, "imixh", "rx_span_kernel")])
 def test_dispatch_boundaries(gpu, monkeypatch, n, size, kernel):
     """The automatic kernel choice (mtcp_gpu.hip pick_sched) on both sides of
     each boundary it draws — small frames: wave up to 2 048, quad up to
     128 K, then quads for 64 B slots and the span kernel for larger ones; MTU
     frames: wave up to 8 192, row up to 32 K, 8 lanes per packet up to 64 K
     (slots <= 2 KiB), rx_kernel above; 4 KiB slots and up: wave up to 64 K;
-    past 32 K frames of <= 640 B slots the span kernel — each the kernel it
+    past 32 K frames of <= 640 B slots the span kernel; 2 KiB slots wave up
+    to 16 K; and, with a size hint saying the batch is of one size class
+    (mtcp_gpu_rx_chunk_hint_dev), 8 lanes per packet for 256-640 B slots up
+    to 64 K frames and the span kernel for 768 B slots past 64 K, while a
+    hinted mix (bimodal, IMIX) keeps the mix's kernel — each the kernel it
     should be, and equal to the oracle."""
     monkeypatch.delenv("MTCP_GPU_SCHED", raising=False)
     seed = 67
+    hinted = isinstance(size, str) and size.endswith("h")
+    size = size[:-1] if hinted else size
     if size == "imix":
         desc, nbytes = pktgen.layout_from_lengths(imix_lengths(n, seed), 6)
     else:
-        desc, nbytes = pktgen.layout(n, size, 6, seed)
+        desc, nbytes = pktgen.layout(n, size if size == "bimodal" else int(size), 6, seed)
     buf = np.zeros(nbytes, np.uint8)
     oracle.pktgen(buf, desc, 6, seed, 0)
     want = oracle.rx_chunk(buf, desc, 6)
+    hint = (int(desc["len"].min()), int(desc["len"].max())) if hinted else None
     with gpu.Context(0) as ctx:
-        assert_same(run_rx_dev(ctx, buf, desc, 6), want, f"auto {size} x {n}")
+        assert_same(run_rx_dev(ctx, buf, desc, 6, hint=hint), want, f"auto {size} x {n} hint {hint}")
         assert ctx.last_kernel.startswith(kernel), ctx.last_kernel
 
 
@@ -328,6 +341,11 @@ def test_tx_fill_ptrs_golden(gpu, golden, monkeypatch, sched):
         host = golden.buf.copy()
         assert ctx.tx_fill_ptrs(host, offs, golden.desc["len"]) == golden.manifest["tx_filled"]
         assert np.array_equal(host, want)
+        # the bounded form (gpu_module.c's send_pkts) fills the same bytes
+        host = golden.buf.copy()
+        assert ctx.tx_fill_ptrs(host, offs, golden.desc["len"], timeout_us=2_000_000) == \
+            golden.manifest["tx_filled"]
+        assert np.array_equal(host, want)
         # a 64-frame burst (MAX_PKT_BURST) at 2-byte-aligned starts
         buf2, d2 = repack(golden.buf, golden.desc[:64], 0, _even_phase)
         w2 = buf2.copy()
@@ -358,3 +376,52 @@ def test_reserve_and_rxq_after_host_calls(gpu, golden):
         ctx.reserve(0, 0)
         got = ctx.rx_chunk(golden.buf, golden.desc, 0)
         assert not compare_results(got, golden)
+
+
+def max_length_frames(n=64, seed=7):
+    """n IPv4/TCP frames of 65 535 B down to 65 472 B (tot_len up to 65 521,
+    the u16 limit of desc.len) whose payload is all 0xFF, the checksums
+    filled by the oracle's tx fill and every eighth frame's payload bit
+    flipped after it: the largest one's-complement sums any kernel meets
+    (rx_span_kernel's per-frame LDS sum of 4 096 chunks x up to 524 280 is
+    about 2.15e9, below 2^32)."""
+    rng = np.random.default_rng(seed)
+    lens = (65535 - np.arange(n)).astype(np.uint16)
+    slots = (lens.astype(np.int64) + 63) & ~63
+    offs = np.concatenate([[0], np.cumsum(slots)[:-1]])
+    buf = np.full(int(slots.sum()), 0xFF, np.uint8)
+    desc = np.zeros(n, DESC_DTYPE)
+    desc["offset"] = (offs >> 6).astype(np.uint32)
+    desc["len"] = lens
+    for i in range(n):
+        f = buf[offs[i]:offs[i] + int(lens[i])]
+        f[0:12] = rng.integers(0, 256, 12, dtype=np.uint8)
+        f[12:14] = (0x08, 0x00)
+        tot = int(lens[i]) - 14
+        f[14:34] = (0x45, 0, tot >> 8, tot & 0xFF, 0, 1, 0x40, 0, 64, 6, 0, 0, *rng.integers(0, 256, 8))
+        f[34:54] = (*rng.integers(0, 256, 12), 0x50, 0x10, 0xFF, 0xFF, 0, 0, 0, 0)
+    assert oracle.tx_fill(buf, desc, 6) == n
+    for i in range(0, n, 8):
+        buf[offs[i] + 60000] ^= 0x10
+    return buf, desc
+
+
+@pytest.mark.parametrize("sched", SCHEDS)
+def test_max_length_frames_every_schedule(gpu, monkeypatch, sched):
+    """frames at the u16 length limit, all-0xFF payload, through
+    every kernel (a forced span included) and the pointer path: equal to the
+    oracle, TCP_OK except the flipped ones (TCP_CSUM_BAD)."""
+    buf, desc = max_length_frames()
+    want = oracle.rx_chunk(buf, desc, 6)
+    assert (want["verdict"][::8] == 9).all() and (np.delete(want["verdict"], np.s_[::8]) == 0).all()
+    n = len(desc)
+    with ctx_for(gpu, monkeypatch, sched) as ctx:
+        assert_same(run_rx_dev(ctx, buf, desc, 6), want, f"{sched} max-length chunk")
+        b = to_dev(buf)
+        pd = desc.copy()
+        pd["offset"] = (desc["offset"].astype(np.int64) << 6).astype(np.uint32)
+        ptrs, lens = ptr_burst(b, pd)
+        out = dev_results(n)
+        ctx.rx_ptrs_dev(ptrs, lens, n, out)
+        torch.cuda.synchronize()
+        assert_same(out.cpu().numpy().view(RESULT_DTYPE), want, f"{sched} max-length pointers")

@@ -150,3 +150,18 @@ def test_cpu_baseline_at_n_ranks():
     slowest = max(x["seconds"] for x in r["per_rank"])
     assert abs(r["value"] - 2 * 2048 * 1500 / slowest / 1e9) < 0.01 * r["value"]   # seconds rounded to 1 us
     assert r["value"] <= sum(x["GB/s"] for x in r["per_rank"]) + 1e-3
+
+
+def test_split_cpus_eight_shares(tmp_path):
+    """bench.py --gpus 8: the ranks whose GPUs share a node split its cores.
+    An 8-GPU node with 4 GPUs per socket (64 cores + SMT per socket): each of
+    the 4 ranks gets 16 whole cores; the one-GPU box's 16-cpu share (8 cores
+    + SMT) rehearsing 8 ranks: one whole core each, disjoint."""
+    _fake_topology(tmp_path, 128, 2)
+    socket0 = set(range(64)) | set(range(128, 192))
+    shares = [shard.split_cpus(socket0, i, 4, str(tmp_path)) for i in range(4)]
+    assert set().union(*shares) == socket0 and all(len(s) == 32 for s in shares)
+    assert all(not (a & b) for i, a in enumerate(shares) for b in shares[i + 1:])
+    box = set(range(8)) | set(range(128, 136))
+    shares = [shard.split_cpus(box, i, 8, str(tmp_path)) for i in range(8)]
+    assert shares == [{i, 128 + i} for i in range(8)]

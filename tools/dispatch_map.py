@@ -16,17 +16,23 @@ def main():
     worst = []
     for (n, size) in sorted(rows, key=lambda k: (k[0], k[1])):
         r = rows[(n, size)]
-        if "auto" not in r:
+        # the automatic choice with the size hint when the run has it (what an
+        # io_module's rxq passes), else without
+        key = "auto_hint" if "auto_hint" in r else "auto"
+        if key not in r:
             continue
-        forced = {k: v for k, v in r.items() if k != "auto"}
+        forced = {k: v for k, v in r.items() if not k.startswith("auto")}
         best = min(forced.items(), key=lambda kv: kv[1]["us_per_launch"])
-        a = r["auto"]
+        a = r[key]
         ratio = a["us_per_launch"] / best[1]["us_per_launch"]
         same = len({v["records_sha"] for v in r.values()}) == 1
         worst.append(ratio)
-        print(json.dumps({"n": n, "size": size, "auto_kernel": a["kernel"], "auto_us": a["us_per_launch"],
-                          "best": best[0], "best_us": best[1]["us_per_launch"], "auto_over_best": round(ratio, 3),
-                          "records_identical": same}))
+        row = {"n": n, "size": size, "auto": key, "auto_kernel": a["kernel"], "auto_us": a["us_per_launch"],
+               "best": best[0], "best_us": best[1]["us_per_launch"], "auto_over_best": round(ratio, 3),
+               "records_identical": same}
+        if key == "auto_hint" and "auto" in r:
+            row["unhinted_kernel"], row["unhinted_us"] = r["auto"]["kernel"], r["auto"]["us_per_launch"]
+        print(json.dumps(row))
     if worst:
         print(json.dumps({"cells": len(worst), "auto_within_5pct": sum(w <= 1.05 for w in worst),
                           "auto_within_10pct": sum(w <= 1.10 for w in worst), "worst": round(max(worst), 3)}))

@@ -6,10 +6,12 @@
 # python3 tools/dispatch_map.py gpurun_out/dispatch_map.jsonl
 set -o pipefail
 SIZES="64 128 256 512 768 1024 1500 2048 4096 9000 bimodal imix"
+OUT=${OUT:-gpurun_out/dispatch_map.jsonl}
 for n in ${NS:-4096 16384 32768 65536 131072 262144 1048576}; do
-  for s in ${SCHEDS:-auto wave row quad oct span big}; do
-    if [ $s = auto ]; then unset MTCP_GPU_SCHED; else export MTCP_GPU_SCHED=$s; fi
-    timeout -k 10 150 python -u tools/size_sweep.py --n $n --no-ceiling $SIZES >> gpurun_out/dispatch_map.jsonl 2>/dev/null || exit 1
+  for s in ${SCHEDS:-auto auto_hint wave row quad oct span big}; do
+    hint=""
+    case $s in auto) unset MTCP_GPU_SCHED ;; auto_hint) unset MTCP_GPU_SCHED; hint=--hint ;; *) export MTCP_GPU_SCHED=$s ;; esac
+    timeout -k 10 150 python -u tools/size_sweep.py --n $n --no-ceiling $hint $SIZES >> $OUT 2>/dev/null || exit 1
   done
   echo "n=$n done"
 done

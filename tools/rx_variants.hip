@@ -775,6 +775,11 @@ int main(int argc, char **argv) {
         // the ladder of the shipped schedule: phase 1 alone, + records
         vs.push_back({"abl1_b16_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 0, 16>, 2});
         vs.push_back({"abl1_b16_rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6, false, 1, 8, 16>, 2});
+        // round 5: phase 1 without its LDS header / tail copies (every
+        // bank-conflicting ds_write of the size-sorted rounds): the most those
+        // copies, and so their conflicts, can cost (records wrong)
+        vs.push_back({"abl2_b16_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 2, 0, 16>, 2});
+        vs.push_back({"abl3_b16_rss_sorted6_nostore_cu2", rx_kernel<kRxChunk, true, 6, false, 3, 0, 16>, 2});
         vs.push_back({"rss_sorted6_cu2", rx_kernel<kRxChunk, true, 6>, 2});
         vs.push_back({"b16_rss_sorted6_cmp_cu2", rx_kernel<kRxChunk, true, 6, false, 0, 8, 16, true, 6, false, false, 0, 4, 0, true>, 2});
         vs.push_back({"ldsrun12_cu2", lds_run_walk<12>, 2});

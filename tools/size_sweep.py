@@ -5,8 +5,10 @@ in HBM, 50 back-to-back mtcp_gpu_rx_chunk_dev launches timed with HIP events
 on the launch stream, next to the box's read ceiling on the same buffer
 (tools/libstream_ceiling.so).  One JSON line per size: the kernel the
 dispatcher picked, its time, Σ L / t against 8 TB/s and against the stream.
-  usage: python tools/size_sweep.py [--n N] [--no-ceiling] [--ptrs] [--compact] [sizes...]
+  usage: python tools/size_sweep.py [--n N] [--no-ceiling] [--ptrs] [--compact] [--hint] [sizes...]
   --ptrs: the same frames as a pointer burst (mtcp_gpu_rx_ptrs_dev).
+  --hint: pass the batch's (min, max) frame length (mtcp_gpu_rx_chunk_hint_dev),
+  as an io_module's rxq does.
   --compact: 16 B records (MTCP_GPU_F_COMPACT) instead of 40 B.
   sizes: bytes, or "bimodal" (C3's 64 / 1500 B mix) or "imix" (64 / 576 /
   1500 B, 7 : 4 : 1); --n fixes the batch (default ~1.5 GB of slots, <= 8 M).
@@ -46,10 +48,12 @@ def lengths(n, size):
 
 def main():
     args = sys.argv[1:]
-    fixed_n, ceiling, ptrs, compact = None, True, False, False
-    while args[:1] in (["--n"], ["--no-ceiling"], ["--ptrs"], ["--compact"]):
+    fixed_n, ceiling, ptrs, compact, hinted = None, True, False, False, False
+    while args[:1] in (["--n"], ["--no-ceiling"], ["--ptrs"], ["--compact"], ["--hint"]):
         if args[0] == "--n":
             fixed_n, args = int(args[1]), args[2:]
+        elif args[0] == "--hint":
+            hinted, args = True, args[1:]
         elif args[0] == "--ptrs":
             ptrs, args = True, args[1:]
         elif args[0] == "--compact":
@@ -74,7 +78,8 @@ def main():
             ln = torch.from_numpy(desc["len"].view(np.int16).copy()).to(dev)
             launch = lambda ctx: ctx.rx_ptrs_dev(p, ln, n, out, stream=stream)  # noqa: E731
         else:
-            launch = lambda ctx: ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream)  # noqa: E731
+            hint = (int(desc["len"].min()), int(desc["len"].max())) if hinted else None
+            launch = lambda ctx: ctx.rx_chunk_dev(buf, d, n, 6, out, stream=stream, hint=hint)  # noqa: E731
         with gpu.Context(0, compact=compact) as ctx:
             ceil = ceiling_us(buf, nbytes, stream) if ceiling else float("nan")
             for _ in range(5):
@@ -92,7 +97,7 @@ def main():
             got = out.clone()
         fb = int(desc["len"].astype(np.int64).sum())
         print(json.dumps({"probe": "size_sweep", "mode": "ptrs" if ptrs else "chunk",
-                          "sched": os.environ.get("MTCP_GPU_SCHED", "auto"),
+                          "sched": os.environ.get("MTCP_GPU_SCHED", "auto") + ("_hint" if hinted else ""),
                           "frame_size": size, "frames": n, "kernel": kernel,
                           "us_per_launch": round(us, 2), "GBs": round(fb / us / 1e3, 1),
                           "gpkt_per_s": round(n / us / 1e3, 3), "frac_of_8TBs": round(fb / us / 8e6, 4),
