@@ -116,7 +116,7 @@ def imix_lengths(n, seed):
     (8192, 1500, "rx_wave"), (8193, 1500, "rx_group_kernel<row"), (32768, 512, "rx_group_kernel<row"),
     (32769, 512, "rx_span_kernel"), (32769, 640, "rx_span_kernel"), (32769, 704, "rx_group_kernel<oct"),
     (65536, 1500, "rx_group_kernel<oct"), (65537, 1500, "rx_kernel"), (65536, 4096, "rx_wave"),
-    (65537, 4096, "rx_kernel"), (16384, 4032, "rx_group_kernel<row"),
+    (65537, 4096, "rx_kernel"), (16384, 4032, "rx_wave"), (32768, 4032, "rx_group_kernel<row"),
     ((1 << 18) + 3, "imix", "rx_span_kernel"), (16384, 2048, "rx_wave"), (16385, 2048, "rx_group_kernel<row"),
     # with the caller's size hint (mtcp_gpu_rx_chunk_hint_dev): one size class
     ((1 << 16), "256h", "rx_group_kernel<oct"), ((1 << 16) + 1, "256h", "rx_span_kernel"),

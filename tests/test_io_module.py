@@ -301,7 +301,7 @@ def test_production_build_has_no_fault_injection(tmp_path):
                     "-I" + os.path.join(ROOT, "tests", "c", "mtcp_double"), "-I" + os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "mtcp_amd", "io_module", "gpu_module.c"), "-o", str(obj)], check=True)
     data = obj.read_bytes()
-    for var in (b"MTCP_GPU_FAIL_AFTER", b"MTCP_GPU_STALL_AFTER", b"MTCP_GPU_STALL_US"):
+    for var in (b"MTCP_GPU_FAIL_AFTER", b"MTCP_GPU_STALL_AFTER", b"MTCP_GPU_TX_STALL_AFTER", b"MTCP_GPU_STALL_US"):
         assert var not in data, var
     assert b"MTCP_GPU_THREADS" in data and b"MTCP_GPU_WAIT_TIMEOUT_MS" in data
     undef = subprocess.run(["nm", "-u", str(obj)], capture_output=True, text=True, check=True).stdout

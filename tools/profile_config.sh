@@ -14,7 +14,7 @@ case "$cfg" in
 esac
 sha256sum mtcp_amd/lib/libmtcp_gpu.so | cut -d' ' -f1 > "$out/lib.sha256"   # the build profiled
 python3 -c "from mtcp_amd import _codeobj; print(_codeobj.rx_source_key())" > "$out/rx_source.key"
-b="python3 bench.py $bargs --steps 200 --warmup 20 --cpu-baseline off --pcie off --small-batch off --ceiling off"
+b="python3 bench.py $bargs --steps 200 --warmup 20 --cpu-baseline off --pcie off --small-batch off --ceiling off --c4-per-gpu off"
 timeout -s KILL 150 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$out/trace" -o run -- $b > "$out/trace.log" 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$out/fetch" -o run -- $b > "$out/fetch.log" 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d "$out/write" -o run -- $b > "$out/write.log" 2>&1 || exit $?
