@@ -309,6 +309,16 @@ int pick_sched(const mtcp_gpu_ctx *ctx, uint32_t n, uint64_t slot, bool small_on
             big = kSchedSpan;
         if (slot < 256) {
             s = n <= 2048 ? kSchedWave : n <= (1u << 17) ? kSchedQuad : big;
+        } else if (narrow && slot <= kSpanUpToSlot && n > 2048 && n <= kOctUpToPkts) {
+            // one size class of 256-640 B slots: 8 lanes per packet from 4 K
+            // frames on (4 K x 256 / 512 B 3.34 / 3.61 us against the wave
+            // kernel's 3.96 / 3.98, 32 K x 256 B 4.20 against the row
+            // kernel's 4.82; an IMIX of 4 K frames keeps the wave kernel,
+            // 3.86 against 5.06: profiles/r5/dispatch_map.jsonl)
+            s = kSchedOct;
+        } else if (narrow && slot <= 320 && n <= (1u << 17)) {
+            // 128 K frames of 256 B: quads, 8.55 against the span kernel's 9.27 us
+            s = kSchedQuad;
         } else if (slot >= 4096) {
             s = n <= (1u << 16) || (narrow && slot <= kWaveNarrowUpToSlot && n >= kWaveNarrowFromPkts)
                     ? kSchedWave : kSchedBig;

@@ -119,7 +119,9 @@ def imix_lengths(n, seed):
     (65537, 4096, "rx_kernel"), (16384, 4032, "rx_wave"), (32768, 4032, "rx_group_kernel<row"),
     ((1 << 18) + 3, "imix", "rx_span_kernel"), (16384, 2048, "rx_wave"), (16385, 2048, "rx_group_kernel<row"),
     # with the caller's size hint (mtcp_gpu_rx_chunk_hint_dev): one size class
-    ((1 << 16), "256h", "rx_group_kernel<oct"), ((1 << 16) + 1, "256h", "rx_span_kernel"),
+    ((1 << 16), "256h", "rx_group_kernel<oct"), ((1 << 16) + 1, "256h", "rx_group_kernel<quad"),
+    ((1 << 17) + 1, "256h", "rx_span_kernel"), (4096, "512h", "rx_group_kernel<oct"), (2048, "512h", "rx_wave"),
+    (16384, "256h", "rx_group_kernel<oct"), (4096, "imixh", "rx_wave"), ((1 << 16) + 1, "512h", "rx_span_kernel"),
     ((1 << 16), "512h", "rx_group_kernel<oct"), ((1 << 16), 512, "rx_span_kernel"),
     ((1 << 16) + 1, "768h", "rx_span_kernel"), ((1 << 16) + 1, 768, "rx_kernel"),
     ((1 << 16) + 1, "1024h", "rx_kernel"), ((1 << 17) + 1, "bimodalh", "rx_kernel<sorted>"),
@@ -132,10 +134,11 @@ def test_dispatch_boundaries(gpu, monkeypatch, n, size, kernel):
     (slots <= 2 KiB), rx_kernel above; 4 KiB slots and up: wave up to 64 K;
     past 32 K frames of <= 640 B slots the span kernel; 2 KiB slots wave up
     to 16 K; and, with a size hint saying the batch is of one size class
-    (mtcp_gpu_rx_chunk_hint_dev), 8 lanes per packet for 256-640 B slots up
-    to 64 K frames and the span kernel for 768 B slots past 64 K, while a
-    hinted mix (bimodal, IMIX) keeps the mix's kernel — each the kernel it
-    should be, and equal to the oracle."""
+    (mtcp_gpu_rx_chunk_hint_dev), 8 lanes per packet for 256-640 B slots
+    from 4 K to 64 K frames, quads for 256 B slots up to 128 K, the span
+    kernel for 768 B slots past 64 K, while a hinted mix (bimodal, IMIX)
+    keeps the mix's kernel — each the kernel it should be, and equal to the
+    oracle."""
     monkeypatch.delenv("MTCP_GPU_SCHED", raising=False)
     seed = 67
     hinted = isinstance(size, str) and size.endswith("h")
