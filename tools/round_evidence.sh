@@ -27,7 +27,10 @@ bash tools/gpu_steps.sh \
   "bf1|150|python bench.py --config f1" \
   "bf3|150|python bench.py --config f3" \
   "bf4|150|python bench.py --config f4" \
-  "c2x5|300|for i in 1 2 3 4 5; do python bench.py --steps 20 --warmup 5 --cpu-baseline off --pcie off --small-batch off || exit 1; done" \
-  "bn2|200|MTCP_BENCH_DEVICE=0 python bench.py --gpus 2 --steps 20 --warmup 5 --pcie off" \
+  "c2x5|300|for i in 1 2 3 4 5; do python3 bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; done" \
+  "bn8|300|MTCP_BENCH_DEVICE=0 python3 bench.py --gpus 8 --per-gpu 131072 --steps 20 --warmup 5" \
+  "txhang|120|MTCP_GPU_TX=1 MTCP_GPU_PIPELINE=1 MTCP_GPU_TX_STALL_AFTER=2 MTCP_GPU_STALL_US=1500000 MTCP_GPU_WAIT_TIMEOUT_MS=100 oracle/_ref/dropin_tx /tmp/txhang.bin 4096 observe" \
+  "txsw|120|MTCP_GPU_TX=0 oracle/_ref/dropin_tx /tmp/txsw.bin 4096 observe && MTCP_GPU_TX=1 oracle/_ref/dropin_tx /tmp/txgpu.bin 4096 observe && cmp /tmp/txhang.bin /tmp/txsw.bin && cmp /tmp/txgpu.bin /tmp/txsw.bin && echo tx-frames-identical" \
+  "dmap|400|OUT=gpurun_out/dispatch_map.jsonl bash tools/dispatch_map.sh" \
   "pr|240|bash tools/profile_rows.sh gpurun_out/prof_rows" \
   "wp|120|./tools/wave_probe 1500 64 1024 4096 16384 32768 && ./tools/wave_probe 9000 64 4096 16384 && ./tools/wave_probe 64 64 4096 16384 65536"
