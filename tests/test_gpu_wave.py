@@ -428,3 +428,28 @@ def test_max_length_frames_every_schedule(gpu, monkeypatch, sched):
         ctx.rx_ptrs_dev(ptrs, lens, n, out)
         torch.cuda.synchronize()
         assert_same(out.cpu().numpy().view(RESULT_DTYPE), want, f"{sched} max-length pointers")
+
+
+@pytest.mark.parametrize("n,size,hint", [
+    (1 << 16, "bimodal", (700, 800)),       # a mix claimed uniform: 8 lanes per packet on it
+    ((1 << 17) + 1, "imix", (700, 800)),    # the span kernel on an IMIX claimed uniform 768 B
+    (4096, "bimodal", (256, 300)),          # 8 lanes at 4 K
+    ((1 << 16) + 1, 256, (0, 0)),           # empty hint
+    ((1 << 16) + 1, 256, (900, 100)),       # min > max
+    ((1 << 16) + 1, 256, (1, 65535)),       # a hint wider than the batch
+])
+def test_records_never_depend_on_the_hint(gpu, monkeypatch, n, size, hint):
+    """mtcp_gpu_size_hint only chooses a kernel: a hint that is wrong, empty
+    or inverted still gives the oracle's records, byte for byte (every
+    kernel is exact for any frame mix; include/mtcp_gpu.h)."""
+    monkeypatch.delenv("MTCP_GPU_SCHED", raising=False)
+    seed = 71
+    if size == "imix":
+        desc, nbytes = pktgen.layout_from_lengths(imix_lengths(n, seed), 6)
+    else:
+        desc, nbytes = pktgen.layout(n, size, 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    want = oracle.rx_chunk(buf, desc, 6, oracle.rss_cfg(None, 8, 1))
+    with gpu.Context(0, rss=True, rss_queues=8, rss_endian=True) as ctx:
+        assert_same(run_rx_dev(ctx, buf, desc, 6, hint=hint), want, f"{size} x {n} hint {hint}")

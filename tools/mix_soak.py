@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Size-mix soak (a checking tool, not product code): large batches of
 IMIX, bimodal, uniform mid-size and random-length frames through the
-automatic dispatch and every forced kernel, each compared with the oracle
+automatic dispatch (without and with the size hint) and every forced
+kernel, each compared with the oracle
 field by field (40 B records, RSS on).  One JSON line per batch.
   usage: python tools/mix_soak.py [n]"""
 import json
@@ -17,7 +18,7 @@ sys.path.insert(0, ROOT)
 import oracle  # noqa: E402  (the checker)
 from mtcp_amd import RESULT_DTYPE, gpu, pktgen  # noqa: E402
 
-SCHEDS = ("auto", "wave", "row", "quad", "oct", "span", "big")
+SCHEDS = ("auto", "auto_hint", "wave", "row", "quad", "oct", "span", "big")
 
 
 def lengths(kind, n, rng):
@@ -34,7 +35,7 @@ def lengths(kind, n, rng):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
     rng = np.random.default_rng(2024)
-    for kind in ("imix", "random", "bimodal", "128", "384", "768"):
+    for kind in ("imix", "random", "bimodal", "128", "256", "384", "512", "768"):
         t0 = time.time()
         desc, nbytes = pktgen.layout_from_lengths(lengths(kind, n, rng), 6)
         buf = np.zeros(nbytes, np.uint8)
@@ -45,13 +46,15 @@ def main():
         d = torch.from_numpy(desc.view(np.uint8).copy()).to("cuda:0")
         bad, kernels = {}, {}
         for sched in SCHEDS:
-            if sched == "auto":
+            if sched.startswith("auto"):
                 os.environ.pop("MTCP_GPU_SCHED", None)
             else:
                 os.environ["MTCP_GPU_SCHED"] = sched
             out = torch.full((n * 40,), 0xEE, dtype=torch.uint8, device="cuda:0")
             with gpu.Context(0, rss=True, rss_queues=8, rss_endian=True) as ctx:
-                ctx.rx_chunk_dev(b, d, n, 6, out)
+                # auto_hint: the batch's true {min, max} length (mtcp_gpu_size_hint)
+                hint = (int(desc["len"].min()), int(desc["len"].max())) if sched == "auto_hint" else None
+                ctx.rx_chunk_dev(b, d, n, 6, out, hint=hint)
                 torch.cuda.synchronize()
                 kernels[sched] = ctx.last_kernel
             got = out.cpu().numpy().view(RESULT_DTYPE)
