@@ -788,6 +788,11 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     device = int(os.environ.get("MTCP_BENCH_DEVICE", local_rank))
+    if "MTCP_BENCH_DEVICE" not in os.environ and device >= torch.cuda.device_count() == 1:
+        # a launcher that gives each rank only its own GPU (HIP_VISIBLE_DEVICES
+        # per rank): that one device is this rank's (device_count() does not
+        # initialise HIP on this image)
+        device = 0
     torch.cuda.set_device(device)
     from mtcp_amd import gpu   # loads libmtcp_gpu.so (raises if not built)
     host_cpus = bind_to_device(device, args.numa, world, rank)
