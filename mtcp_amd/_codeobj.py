@@ -6,7 +6,7 @@ profile records two keys:
   lib_sha256     the exact libmtcp_gpu.so that was profiled;
   rx_source_key  the sources that decide the rx kernels' code and their
                  dispatch (rx_kernels.hpp, rx_wave.hpp — C1's quad kernel —, rx_span.hpp,
-                 mtcp_gpu.hip, include/mtcp_gpu.h, the Makefile's flags).
+                 mtcp_gpu.hip, dispatch.hpp, include/mtcp_gpu.h, the Makefile's flags).
 bench.py uses the figure when the loaded library is the profiled one, or
 when it differs only outside those sources (e.g. a small-batch kernel or
 host-path change), and says which; otherwise the figure is reported stale.
@@ -20,7 +20,7 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RX_SOURCES = ("mtcp_amd/csrc/rx_kernels.hpp", "mtcp_amd/csrc/rx_wave.hpp", "mtcp_amd/csrc/rx_span.hpp",
-              "mtcp_amd/csrc/mtcp_gpu.hip", "include/mtcp_gpu.h", "Makefile")
+              "mtcp_amd/csrc/mtcp_gpu.hip", "mtcp_amd/csrc/dispatch.hpp", "include/mtcp_gpu.h", "Makefile")
 
 
 def rx_source_key(root: str = ROOT) -> str:
