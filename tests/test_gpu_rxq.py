@@ -229,3 +229,50 @@ def test_tx_fill_ptrs_for_gives_up_and_abandons(golden):
     with gpu.Context(0) as fresh:
         assert fresh.tx_fill_ptrs(host, offs, part["len"], timeout_us=2_000_000) > 0
         assert np.array_equal(host, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,kernel", [(512, "rx_group_kernel<oct>"), ("bimodal", "rx_wave_kernel")])
+def test_rxq_passes_its_size_hint(size, kernel):
+    """An rxq sees every length at push and launches its aggregate with the
+    aggregate's {min, max} (mtcp_gpu_rx_chunk_hint_dev): 4 096 frames of
+    512 B, with NULL pushes between them (the wrapped backend's own NULLs,
+    length 0, not counted in the hint), take the uniform kernel (8 lanes per
+    packet); a 64 / 1500 B aggregate keeps the mix's (a wave per packet).
+    Every served record equals the oracle's."""
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    from mtcp_amd import gpu, pktgen
+    from mtcp_amd._lib import lib
+    L = lib()
+    n, seed = 4096, 29
+    desc, nbytes = pktgen.layout(n, size, 6, seed)
+    buf = np.zeros(nbytes, np.uint8)
+    oracle.pktgen(buf, desc, 6, seed, 0)
+    want = oracle.rx_chunk(buf, desc, 6)
+    base = buf.ctypes.data
+    with gpu.Context(0) as ctx:
+        q = ctypes.c_void_p()
+        assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, n + 64, (n + 64) * 2048) == 0
+        try:
+            null_at = set(range(0, n, 97))
+            order = []
+            for i, d in enumerate(desc):
+                if i in null_at:
+                    assert L.mtcp_gpu_rxq_push(q, None, 0) == 0
+                    order.append(-1)
+                assert L.mtcp_gpu_rxq_push(q, base + (int(d["offset"]) << 6), int(d["len"])) == 0
+                order.append(i)
+            n_done = ctypes.c_uint32()
+            assert L.mtcp_gpu_rxq_flush(q, ctypes.byref(n_done)) == 0 and n_done.value == len(order)
+            assert ctx.last_kernel.startswith(kernel), ctx.last_kernel
+            for j, i in enumerate(order):
+                ln, res = ctypes.c_uint16(), ctypes.c_void_p()
+                L.mtcp_gpu_rxq_get(q, j, ctypes.byref(ln), ctypes.byref(res))
+                got = np.frombuffer(ctypes.string_at(res.value, 40), dtype=RESULT_DTYPE)[0]
+                if i < 0:
+                    assert got["verdict"] == V_TRUNCATED         # a 0-byte frame (the oracle's too)
+                else:
+                    assert got.tobytes() == want[i].tobytes(), i
+        finally:
+            L.mtcp_gpu_rxq_destroy(q)
