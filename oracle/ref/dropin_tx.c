@@ -31,9 +31,12 @@
  * each; the symbols tcp_out.c names for the stateful sender (not reached
  * from the standalone builder) are aborting stubs (ref/tx_stubs.c).
  *
- *   dropin_tx OUT N [observe|plain]
+ *   dropin_tx OUT N [observe|plain [nofinal]]
  *     OUT  N records of 2048 B: u16 len, u16 proto, 4 B pad, then the frame
  *          as the NIC sent it
+ *     nofinal  no send_pkts after the last frame: the frames of the last
+ *          partial burst are still recorded when destroy_handle runs (its
+ *          flush fills them); the NIC sends them after the shutdown
  *   prints one JSON line
  */
 #define _GNU_SOURCE
@@ -186,15 +189,16 @@ int main(int argc, char **argv)
     mtcp_manager_t mtcp;
     uint8_t payload[TCP_DEFAULT_MSS + 64];
     uint32_t n, i, tcp_frames = 0, icmp_frames = 0, refused = 0;
-    int observe;
+    int observe, final_send;
     FILE *out;
 
     if (argc < 3) {
-        fprintf(stderr, "usage: dropin_tx OUT N [observe|plain]\n");
+        fprintf(stderr, "usage: dropin_tx OUT N [observe|plain [nofinal]]\n");
         return 1;
     }
     n = (uint32_t)atoi(argv[2]);
     observe = !(argc > 3 && strcmp(argv[3], "plain") == 0);
+    final_send = !(argc > 4 && strcmp(argv[4], "nofinal") == 0);
 
     /* mtcp.conf's one port, one route, one ARP entry (config.c fills these) */
     memcpy(eths[0].haddr, "\x02\x00\x00\x00\x00\x01", 6);
@@ -266,11 +270,16 @@ int main(int argc, char **argv)
         if ((i + 1) % BURST == 0)
             send_timed(mtcp, &ctx);                      /* core.c:818-824 */
     }
-    send_timed(mtcp, &ctx);
+    if (final_send)
+        send_timed(mtcp, &ctx);
     {
         double t0 = now_s();
         mtcp->iom->destroy_handle(&ctx);
         g_destroy_s = now_s() - t0;
+    }
+    if (!final_send) {          /* the NIC drains its ring after the shutdown */
+        ctx.io_private_context = g_nic;
+        nic_send(&ctx, 0);
     }
 
     out = fopen(argv[1], "wb");

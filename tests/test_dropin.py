@@ -208,14 +208,14 @@ EXE_TX = os.path.join(ROOT, "oracle", "_ref", "dropin_tx")
 TX_SLOT = 2048
 
 
-def run_dropin_tx(tmp_path, n=4096, tx="1", mode="observe", inject=None):
+def run_dropin_tx(tmp_path, n=4096, tx="1", mode="observe", inject=None, final_send=True):
     if not os.path.exists(EXE_TX):
         pytest.fail("oracle/_ref/dropin_tx not built: `make -C oracle ref` (needs /root/reference)")
-    out = tmp_path / f"tx_{tx}_{mode}_{bool(inject)}.bin"
+    out = tmp_path / f"tx_{tx}_{mode}_{bool(inject)}_{n}_{final_send}.bin"
     env = dict(os.environ, MTCP_GPU_TX=tx, MTCP_GPU_PIPELINE="1")
     env.update(inject or {})
-    p = subprocess.run([EXE_TX, str(out), str(n), mode], capture_output=True, text=True, timeout=300,
-                       env=env)
+    argv = [EXE_TX, str(out), str(n), mode] + ([] if final_send else ["nofinal"])
+    p = subprocess.run(argv, capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     stats = json.loads(p.stdout.strip().splitlines()[-1])
     recs = np.fromfile(out, dtype=np.uint8).reshape(-1, TX_SLOT)
@@ -299,6 +299,38 @@ def test_dropin_tx_gpu_hang_falls_back_to_mtcp(tmp_path):
     assert 0 < stats["tcp_csum_calls"] - stats["tcpip_sw"] <= 64
     assert stats["ioctl_tcpip"] == -1 and stats["ioctl_peek"] == -1
     # bounded: no send_pkts and no shutdown waited for the 1.5 s stall
+    assert stats["max_send_s"] < 0.75, stats
+    assert stats["destroy_s"] < 0.75, stats
+    assert np.array_equal(recs, sw)
+    v, proto = tx_frames_verify(recs)
+    assert (v[proto == 6] == 0).all() and (v[proto == 1] == 6).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stall", [False, True])
+def test_dropin_tx_shutdown_fills_the_last_burst(tmp_path, stall):
+    """Frames recorded after the last send_pkts are filled by destroy_handle
+    (gpu_module.c gpu_destroy_handle -> gpu_tx_flush) before mTCP's shutdown
+    returns: 4 100 frames sent every 64 leave 4 in the NIC's ring, sent after
+    the shutdown (`nofinal`).  On a healthy GPU the shutdown fills them on the
+    GPU (no TCPCalcChecksum at all); when the GPU stalls 1.5 s exactly at
+    that fill (the 65th: MTCP_GPU_TX_STALL_AFTER=64) the shutdown gives up
+    after MTCP_GPU_WAIT_TIMEOUT_MS, fills those 4 frames in software and
+    returns far below the stall.  Either way the frames equal, byte for byte,
+    the ones the reference fills itself in the same run shape."""
+    n = 4100
+    inject = {"MTCP_GPU_TX_STALL_AFTER": "64", "MTCP_GPU_STALL_US": "1500000",
+              "MTCP_GPU_WAIT_TIMEOUT_MS": "100"} if stall else None
+    stats, recs = run_dropin_tx(tmp_path, n=n, tx="1", inject=inject, final_send=False)
+    sw_stats, sw = run_dropin_tx(tmp_path, n=n, tx="0", final_send=False)
+    assert stats["sent"] == stats["frames"] == sw_stats["sent"] == len(recs) == n
+    assert stats["refused"] == 0
+    # mTCP left every TCP frame to the device: the GPU was alive while it built them
+    assert stats["tcpip_zero"] == stats["tcp"] and stats["tcpip_sw"] == 0
+    tail_tcp = int((recs[n - n % 64:, 8 + 23] == 6).sum())
+    assert tail_tcp > 0
+    # software fills: none on a healthy GPU, the shutdown's burst after a stall
+    assert stats["tcp_csum_calls"] == (tail_tcp if stall else 0)
     assert stats["max_send_s"] < 0.75, stats
     assert stats["destroy_s"] < 0.75, stats
     assert np.array_equal(recs, sw)
