@@ -664,14 +664,25 @@ static int32_t gpu_select(struct mtcp_thread_context *ctx)
 static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
 {
     struct gpu_private_context *g = ctx->io_private_context;
-    int i;
+    int i, b;
 
+    /* an aggregate still on the GPU (the pipeline's last one, when mTCP
+     * stops with frames in flight): the same bounded wait as recv_pkts'; a
+     * GPU that does not finish it is abandoned and its staging stays below */
+    for (i = 0; i < MAX_DEVICES && g->gpu; i++)
+        for (b = 0; b < 2 && g->gpu && g->ifq[i]; b++)
+            if (g->ifq[i]->rxq[b] && g->ifq[i]->launched[b]) {
+                if (mtcp_gpu_rxq_wait_for(g->ifq[i]->rxq[b], NULL, g->wait_us) == MTCP_GPU_ETIMEDOUT)
+                    gpu_abandon(g);
+                else
+                    g->ifq[i]->launched[b] = 0;
+            }
     for (i = 0; i < MAX_DEVICES; i++) {
         gpu_tx_flush(g, i);                          /* frames still recorded */
         free(g->txq[i]);
         if (g->ifq[i]) {
             if (!g->hung) {                          /* a hung GPU's staging stays */
-                mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[0]);   /* NULL-safe; waits for its work */
+                mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[0]);   /* NULL-safe; nothing in flight */
                 mtcp_gpu_rxq_destroy(g->ifq[i]->rxq[1]);
             }
             free(g->ifq[i]);

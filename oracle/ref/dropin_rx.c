@@ -28,9 +28,12 @@
  * = &gpu_module_func itself).  Every other symbol the reference objects name
  * is ref_stubs.c's aborting stub.
  *
- *   dropin_rx CHUNK DESC OUT [observe|plain]
+ *   dropin_rx CHUNK DESC OUT [observe|plain [stop]]
  *     CHUNK, DESC  tests/golden/rx_buf.bin, rx_desc.bin (byte offsets)
  *     OUT          one dropin_rec per frame (below)
+ *     stop         mTCP stops as soon as the backend has run dry: the
+ *                  pipelined module's last aggregate is still on the GPU
+ *                  when destroy_handle runs (its frames are never served)
  *   prints one JSON line: counters, nstat.rx_errors[0] / rx_packets[0]
  */
 #define _GNU_SOURCE
@@ -40,6 +43,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/time.h>
+#include <time.h>
 
 #include "mtcp.h"
 #include "eth_in.h"
@@ -255,13 +259,21 @@ static void *slurp(const char *path, size_t *size)
     return p;
 }
 
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 int main(int argc, char **argv)
 {
     size_t nb, nd;
     const uint8_t *chunk;
     const ref_desc_t *desc;
     uint32_t n, seen = 0, served = 0, nulls = 0, changed = 0;
-    int observe, rounds = 0, idle = 0;
+    int observe, stop, rounds = 0, idle = 0;
+    double destroy_s;
     dropin_rec *recs;
     struct mtcp_thread_context ctx;
     mtcp_manager_t mtcp;
@@ -269,10 +281,11 @@ int main(int argc, char **argv)
     FILE *out;
 
     if (argc < 4) {
-        fprintf(stderr, "usage: dropin_rx CHUNK DESC OUT [observe|plain]\n");
+        fprintf(stderr, "usage: dropin_rx CHUNK DESC OUT [observe|plain [stop]]\n");
         return 1;
     }
     observe = !(argc > 4 && strcmp(argv[4], "plain") == 0);
+    stop = argc > 5 && strcmp(argv[5], "stop") == 0;
     chunk = slurp(argv[1], &nb);
     desc = slurp(argv[2], &nd);
     n = (uint32_t)(nd / sizeof(ref_desc_t));
@@ -332,19 +345,26 @@ int main(int argc, char **argv)
             }
         }
         seen += (uint32_t)recv_cnt;
+        if (stop && g_nic.next == g_nic.n)
+            break;                                   /* shut down with frames in flight */
     }
-    mtcp->iom->destroy_handle(&ctx);
+    {
+        double t0 = now_s();
+        mtcp->iom->destroy_handle(&ctx);
+        destroy_s = now_s() - t0;
+    }
 
     out = fopen(argv[3], "wb");
     if (!out || fwrite(recs, sizeof(*recs), n, out) != n) { perror(argv[3]); return 1; }
     fclose(out);
     printf("{\"frames\": %u, \"seen\": %u, \"served\": %u, \"null\": %u, \"changed\": %u, "
            "\"rx_errors\": %llu, \"rx_packets\": %llu, \"rx_bytes\": %llu, \"tcp_csum_calls\": %llu, "
-           "\"rounds\": %d, \"recv_calls\": %d, \"released\": %d, \"observe\": %d}\n",
+           "\"rounds\": %d, \"recv_calls\": %d, \"released\": %d, \"observe\": %d, "
+           "\"destroy_s\": %.6f}\n",
            n, seen, served, nulls, changed, (unsigned long long)mtcp->nstat.rx_errors[0],
            (unsigned long long)mtcp->nstat.rx_packets[0], (unsigned long long)mtcp->nstat.rx_bytes[0],
            (unsigned long long)g_csum_calls,
-           rounds, g_nic.recv_calls, g_nic.released, observe);
+           rounds, g_nic.recv_calls, g_nic.released, observe, destroy_s);
     free(recs);
     free(mtcp);
     return 0;

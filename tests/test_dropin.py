@@ -43,16 +43,17 @@ BR_TCP_OK, BR_IP_SHORT, BR_IP_CSUM_BAD, BR_TCP_LEN_BAD, BR_TCP_CSUM_BAD = 0, 3, 
 NULL = 254
 
 
-def run_dropin(tmp_path, mode="observe", pipeline="1", fail_after=None, inject=None):
+def run_dropin(tmp_path, mode="observe", pipeline="1", fail_after=None, inject=None, stop=False):
     if not os.path.exists(EXE):
         pytest.fail("oracle/_ref/dropin_rx not built: `make -C oracle ref` (needs /root/reference)")
-    out = tmp_path / f"dropin_{mode}_{pipeline}_{fail_after}.bin"
+    out = tmp_path / f"dropin_{mode}_{pipeline}_{fail_after}_{bool(inject)}_{stop}.bin"
     env = dict(os.environ, MTCP_GPU_PIPELINE=pipeline, MTCP_GPU_TX="0")
     if fail_after is not None:
         env["MTCP_GPU_FAIL_AFTER"] = str(fail_after)
     env.update(inject or {})
-    p = subprocess.run([EXE, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"),
-                        str(out), mode], capture_output=True, text=True, timeout=300, env=env)
+    argv = [EXE, os.path.join(GOLD, "rx_buf.bin"), os.path.join(GOLD, "rx_desc.bin"), str(out), mode]
+    p = subprocess.run(argv + (["stop"] if stop else []), capture_output=True, text=True, timeout=300,
+                       env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads(p.stdout.strip().splitlines()[-1]), np.fromfile(out, dtype=REC)
 
@@ -201,6 +202,37 @@ def test_dropin_gpu_failure_falls_back_to_mtcp(tmp_path, golden, pipeline, fault
     want_err = int((ok & np.isin(br, [BR_IP_SHORT, BR_IP_CSUM_BAD, BR_TCP_LEN_BAD,
                                       BR_TCP_CSUM_BAD])).sum()) + ub_err
     assert stats["rx_errors"] == want_err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stall", [False, True])
+def test_dropin_shutdown_with_an_aggregate_in_flight(tmp_path, golden, stall):
+    """mTCP stops while the pipelined module's last aggregate is still on the
+    GPU (`dropin_rx … stop`: the loop ends as soon as the backend has run
+    dry, so the 2 171 frames gathered last are never served).  destroy_handle
+    waits for that aggregate with the same MTCP_GPU_WAIT_TIMEOUT_MS limit as
+    recv_pkts (gpu_module.c gpu_destroy_handle): with a 1.5 s stall queued in
+    front of exactly that launch (MTCP_GPU_STALL_AFTER=1) it gives up after
+    100 ms and abandons the GPU instead of blocking the shutdown.  Every frame
+    served before the stop carries the --disable-hwcsum reference's outcome."""
+    inject = {"MTCP_GPU_WAIT_TIMEOUT_MS": "100"}
+    if stall:
+        inject.update({"MTCP_GPU_STALL_AFTER": "1", "MTCP_GPU_STALL_US": "1500000"})
+    stats, r = run_dropin(tmp_path, "observe", "1", inject=inject, stop=True)
+    n = len(golden.desc)
+    seen = stats["seen"]
+    assert 0 < seen < n and stats["frames"] == n
+    assert stats["destroy_s"] < 0.75, stats
+    # the served prefix: GPU verdicts (dev_ioctl 0), the reference's branches
+    ok = (golden.meta["ref_ub"] == 0)[:seen]
+    br = golden.meta["branch"][:seen]
+    rr = r[:seen]
+    asked = rr["ioctl_ip"] != -2
+    assert asked.any() and (rr["ioctl_ip"][asked] == 0).all()
+    served = rr["branch"] != NULL
+    assert np.array_equal(rr["branch"][served & ok], br[served & ok])
+    assert set(br[~served & ok].tolist()) <= {BR_IP_CSUM_BAD, BR_TCP_CSUM_BAD}
+    assert stats["tcp_csum_calls"] == 0
 
 
 # ---- the tx side: SendTCPPacketStandalone / IPOutputStandalone ----------------
