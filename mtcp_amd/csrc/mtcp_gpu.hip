@@ -19,6 +19,7 @@
 #include "dispatch.hpp"
 #include "flow_kernels.hpp"
 #include "host_copy.hpp"
+#include "park.hpp"
 #include "rx_kernels.hpp"
 #include "rx_span.hpp"
 
@@ -287,6 +288,20 @@ hipStream_t pick(mtcp_gpu_ctx *ctx, void *stream) {
     return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
 }
 
+// a stage's buffers back to park.hpp (its stream has no work on them)
+void stage_release_buf(Stage &s) {
+    mtcp_park::release(s.d_buf, s.buf_cap, mtcp_park::kDevice);
+    s.d_buf = nullptr;
+    s.buf_cap = 0;
+}
+void stage_release_pkts(Stage &s) {
+    mtcp_park::release(s.d_desc, (size_t)s.pkt_cap * sizeof(mtcp_gpu_desc), mtcp_park::kDevice);
+    mtcp_park::release(s.d_out, (size_t)s.pkt_cap * sizeof(mtcp_gpu_result), mtcp_park::kDevice);
+    s.d_desc = nullptr;
+    s.d_out = nullptr;
+    s.pkt_cap = 0;
+}
+
 int stage_reserve(mtcp_gpu_ctx *ctx, Stage &s, uint64_t bytes, uint32_t pkts) {
     if (ctx->abandoned) return MTCP_GPU_EIO;
     // a stage's stream exists once a host call uses the stage (a context
@@ -294,27 +309,25 @@ int stage_reserve(mtcp_gpu_ctx *ctx, Stage &s, uint64_t bytes, uint32_t pkts) {
     // rxqs, has the one stream of mtcp_gpu_open)
     if (!s.stream && !HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)))
         return MTCP_GPU_EIO;
-    // growing frees buffers that the stage's previous batch may still use:
-    // drain that batch first rather than rely on hipFree's implicit sync
+    // growing releases buffers that the stage's previous batch may still
+    // use: drain that batch first (park.hpp releases without any device wait)
     if ((bytes > s.buf_cap || pkts > s.pkt_cap) && s.stream && !HIP_OK(hipStreamSynchronize(s.stream)))
         return MTCP_GPU_EIO;
     if (bytes > s.buf_cap) {
-        if (s.d_buf) (void)hipFree(s.d_buf);
-        s.d_buf = nullptr;
-        s.buf_cap = 0;
+        stage_release_buf(s);
         const uint64_t cap = (bytes + 4095) & ~4095ull;
-        if (!HIP_OK(hipMalloc(&s.d_buf, cap))) return MTCP_GPU_ENOMEM;
+        if (!HIP_OK(mtcp_park::alloc(&s.d_buf, cap, mtcp_park::kDevice))) return MTCP_GPU_ENOMEM;
         s.buf_cap = cap;
     }
     if (pkts > s.pkt_cap) {
-        if (s.d_desc) (void)hipFree(s.d_desc);
-        if (s.d_out) (void)hipFree(s.d_out);
-        s.d_desc = nullptr;
-        s.d_out = nullptr;
-        s.pkt_cap = 0;
-        if (!HIP_OK(hipMalloc(&s.d_desc, (size_t)pkts * sizeof(mtcp_gpu_desc))) ||
-            !HIP_OK(hipMalloc(&s.d_out, (size_t)pkts * sizeof(mtcp_gpu_result))))
+        stage_release_pkts(s);
+        if (!HIP_OK(mtcp_park::alloc(&s.d_desc, (size_t)pkts * sizeof(mtcp_gpu_desc), mtcp_park::kDevice)))
             return MTCP_GPU_ENOMEM;
+        if (!HIP_OK(mtcp_park::alloc(&s.d_out, (size_t)pkts * sizeof(mtcp_gpu_result), mtcp_park::kDevice))) {
+            mtcp_park::release(s.d_desc, (size_t)pkts * sizeof(mtcp_gpu_desc), mtcp_park::kDevice);
+            s.d_desc = nullptr;
+            return MTCP_GPU_ENOMEM;
+        }
         s.pkt_cap = pkts;
     }
     return MTCP_GPU_OK;
@@ -399,8 +412,8 @@ int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rs
     ctx->sched = sched_from_env();
     int rc = MTCP_GPU_OK;
     if (!HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) ||
-        !HIP_OK(hipMalloc(&ctx->d_rss_tables, sizeof(tables))) ||
-        !HIP_OK(hipMalloc(&ctx->d_count, sizeof(uint32_t))) ||
+        !HIP_OK(mtcp_park::alloc(&ctx->d_rss_tables, sizeof(tables), mtcp_park::kDevice)) ||
+        !HIP_OK(mtcp_park::alloc(&ctx->d_count, sizeof(uint32_t), mtcp_park::kDevice)) ||
         !HIP_OK(hipMemcpy(ctx->d_rss_tables, tables, sizeof(tables), hipMemcpyHostToDevice)))
         rc = MTCP_GPU_ENOMEM;
     if (rc != MTCP_GPU_OK) {
@@ -423,19 +436,21 @@ void mtcp_gpu_close(mtcp_gpu_ctx *ctx) {
     }
     DeviceGuard dg(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    // every buffer goes back to park.hpp: a free here would wait for the
+    // other contexts' work on the device
     for (auto &s : ctx->stage) {
         if (s.stream) {
             (void)hipStreamSynchronize(s.stream);
             (void)hipStreamDestroy(s.stream);
         }
-        if (s.d_buf) (void)hipFree(s.d_buf);
-        if (s.d_desc) (void)hipFree(s.d_desc);
-        if (s.d_out) (void)hipFree(s.d_out);
+        stage_release_buf(s);
+        stage_release_pkts(s);
     }
-    if (ctx->h_gather) (void)hipHostFree(ctx->h_gather);
-    if (ctx->h_gather_desc) (void)hipHostFree(ctx->h_gather_desc);
-    if (ctx->d_rss_tables) (void)hipFree(ctx->d_rss_tables);
-    if (ctx->d_count) (void)hipFree(ctx->d_count);
+    mtcp_park::release(ctx->h_gather, ctx->h_gather_cap, mtcp_park::kHost);
+    mtcp_park::release(ctx->h_gather_desc, (size_t)ctx->h_gather_desc_cap * sizeof(mtcp_gpu_desc),
+                       mtcp_park::kHost);
+    mtcp_park::release(ctx->d_rss_tables, mg::kRssTableWords * sizeof(uint32_t), mtcp_park::kDevice);
+    mtcp_park::release(ctx->d_count, sizeof(uint32_t), mtcp_park::kDevice);
     if (ctx->done_evt) (void)hipEventDestroy(ctx->done_evt);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -460,7 +475,7 @@ int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
     // measured): do that here for the stages the host calls use
     const size_t warm = stages ? (size_t)std::min<uint64_t>(ctx->stage[0].buf_cap, 1ull << 20) : 0;
     void *h = nullptr;
-    if (warm && !HIP_OK(hipHostMalloc(&h, warm, hipHostMallocDefault))) return MTCP_GPU_ENOMEM;
+    if (warm && !HIP_OK(mtcp_park::alloc(&h, warm, mtcp_park::kHost))) return MTCP_GPU_ENOMEM;
     if (h) memset(h, 0, warm);
     bool ok = true;
     for (int i = 0; i < stages && ok && h; ++i) {
@@ -470,7 +485,7 @@ int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
              HIP_OK(hipMemcpyAsync(h, st.d_buf, w, hipMemcpyDeviceToHost, st.stream)) &&
              HIP_OK(hipStreamSynchronize(st.stream));
     }
-    if (h) (void)hipHostFree(h);
+    mtcp_park::release(h, warm, mtcp_park::kHost);
     if (!ok) return MTCP_GPU_EIO;
     // the code object loads on the first launch of any of its kernels
     hipFuncAttributes attr;
@@ -699,18 +714,18 @@ int gather_burst(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) total += ((uint64_t)lens[i] + 63) & ~63ull;
     if (total > ctx->h_gather_cap) {
-        if (ctx->h_gather) (void)hipHostFree(ctx->h_gather);
+        mtcp_park::release(ctx->h_gather, ctx->h_gather_cap, mtcp_park::kHost);
         ctx->h_gather = nullptr;
         ctx->h_gather_cap = 0;
-        if (!HIP_OK(hipHostMalloc(&ctx->h_gather, total, hipHostMallocDefault))) return MTCP_GPU_ENOMEM;
+        if (!HIP_OK(mtcp_park::alloc(&ctx->h_gather, total, mtcp_park::kHost))) return MTCP_GPU_ENOMEM;
         ctx->h_gather_cap = total;
     }
     if (n > ctx->h_gather_desc_cap) {
-        if (ctx->h_gather_desc) (void)hipHostFree(ctx->h_gather_desc);
+        mtcp_park::release(ctx->h_gather_desc, (size_t)ctx->h_gather_desc_cap * sizeof(mtcp_gpu_desc),
+                           mtcp_park::kHost);
         ctx->h_gather_desc = nullptr;
         ctx->h_gather_desc_cap = 0;
-        if (!HIP_OK(hipHostMalloc(&ctx->h_gather_desc, (size_t)n * sizeof(mtcp_gpu_desc),
-                                  hipHostMallocDefault)))
+        if (!HIP_OK(mtcp_park::alloc(&ctx->h_gather_desc, (size_t)n * sizeof(mtcp_gpu_desc), mtcp_park::kHost)))
             return MTCP_GPU_ENOMEM;
         ctx->h_gather_desc_cap = n;
     }
@@ -940,7 +955,7 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues, uint3
     uint8_t *d_mem = nullptr;
     const uint64_t out_off = (qbytes + 4ull * (nb + 1) + 7) & ~7ull;     // 8 B aligned entries
     const uint64_t bytes = out_off + 8ull * std::max(limit, 1u);
-    if (!HIP_OK(hipMalloc(&d_mem, bytes))) return MTCP_GPU_ENOMEM;
+    if (!HIP_OK(mtcp_park::alloc(&d_mem, bytes, mtcp_park::kDevice))) return MTCP_GPU_ENOMEM;
     uint8_t *d_queue = d_mem;
     uint32_t *d_counts = reinterpret_cast<uint32_t *>(d_mem + qbytes);
     mtcp_gpu_addr_entry *d_out = reinterpret_cast<mtcp_gpu_addr_entry *>(d_mem + out_off);
@@ -971,7 +986,7 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues, uint3
         if (rc == MTCP_GPU_OK) *n_found = kept;
     }
     (void)hipStreamSynchronize(st);
-    (void)hipFree(d_mem);
+    mtcp_park::release(d_mem, bytes, mtcp_park::kDevice);
     return rc;
 }
 

@@ -24,6 +24,7 @@
 #include "../../include/mtcp_gpu.h"
 #include "../../include/mtcp_gpu_rxq.h"
 #include "host_copy.hpp"
+#include "park.hpp"
 
 // get_rptr serves frame i; the header of frame i + kServeAhead is fetched
 // meanwhile (the staged frames were written with streaming stores, so each
@@ -43,6 +44,7 @@ struct mtcp_gpu_rxq {
     uint32_t rec = 40;                   // record bytes: 40, or 16 for a compact context
     uint32_t max_pkts = 0;
     uint64_t max_bytes = 0;
+    uint64_t staging = 0;                // bytes of buf and d_buf
     uint32_t n = 0;                      // frames staged
     uint32_t done_n = 0;                 // frames with results
     uint32_t inflight = 0;               // frames of an unfinished flush_async (0: none)
@@ -112,13 +114,16 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     if (const char *e = getenv("MTCP_GPU_SERVE_AHEAD")) q->ahead = (uint32_t)atoi(e);
     if (const char *e = getenv("MTCP_GPU_SERVE_HINT")) q->hint = (uint32_t)atoi(e);
     const uint64_t staging = q->max_bytes + (uint64_t)max_pkts * sizeof(mtcp_gpu_desc);
+    q->staging = staging;
+    // park.hpp: a destroy never waits for other threads' work on the device
+    using mtcp_park::kDevice;
+    using mtcp_park::kHost;
     if (hipEventCreateWithFlags(&q->evt, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc(&q->buf, staging, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&q->desc, (size_t)max_pkts * sizeof(mtcp_gpu_desc), hipHostMallocDefault) !=
-            hipSuccess ||
-        hipHostMalloc(&q->res, (size_t)max_pkts * q->rec, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc(&q->d_buf, staging) != hipSuccess ||
-        hipMalloc(&q->d_out, (size_t)max_pkts * q->rec) != hipSuccess) {
+        mtcp_park::alloc(&q->buf, staging, kHost) != hipSuccess ||
+        mtcp_park::alloc(&q->desc, (size_t)max_pkts * sizeof(mtcp_gpu_desc), kHost) != hipSuccess ||
+        mtcp_park::alloc(&q->res, (size_t)max_pkts * q->rec, kHost) != hipSuccess ||
+        mtcp_park::alloc(&q->d_buf, staging, kDevice) != hipSuccess ||
+        mtcp_park::alloc(&q->d_out, (size_t)max_pkts * q->rec, kDevice) != hipSuccess) {
         mtcp_gpu_rxq_destroy(q);
         return MTCP_GPU_ENOMEM;
     }
@@ -167,11 +172,13 @@ void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q) {
         if (q->inflight) (void)hipEventSynchronize(q->evt);
         (void)hipEventDestroy(q->evt);
     }
-    if (q->buf) (void)hipHostFree(q->buf);
-    if (q->desc) (void)hipHostFree(q->desc);
-    if (q->res) (void)hipHostFree(q->res);
-    if (q->d_buf) (void)hipFree(q->d_buf);
-    if (q->d_out) (void)hipFree(q->d_out);
+    // parked, not freed (park.hpp): hipFree / hipHostFree would wait for
+    // every stream on the device, other threads' hung work included
+    mtcp_park::release(q->buf, q->staging, mtcp_park::kHost);
+    mtcp_park::release(q->desc, (size_t)q->max_pkts * sizeof(mtcp_gpu_desc), mtcp_park::kHost);
+    mtcp_park::release(q->res, (size_t)q->max_pkts * q->rec, mtcp_park::kHost);
+    mtcp_park::release(q->d_buf, q->staging, mtcp_park::kDevice);
+    mtcp_park::release(q->d_out, (size_t)q->max_pkts * q->rec, mtcp_park::kDevice);
     delete q;
 }
 

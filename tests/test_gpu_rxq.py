@@ -276,3 +276,62 @@ def test_rxq_passes_its_size_hint(size, kernel):
                     assert got.tobytes() == want[i].tobytes(), i
         finally:
             L.mtcp_gpu_rxq_destroy(q)
+
+
+@pytest.mark.gpu
+def test_a_shutdown_does_not_wait_for_another_contexts_work(golden):
+    """Two mTCP threads on one GPU: thread A's context has 1 s of work queued
+    (mtcp_gpu_debug_stall), thread B creates an rxq, checks a batch, destroys
+    the rxq, closes its context, and a third thread opens and reserves one.
+    None of B's or C's calls waits for A: the library parks its buffers
+    (mtcp_amd/csrc/park.hpp) instead of hipFree / hipHostFree, which wait for
+    every stream on the device (tools/free_sync_probe.py; before parking B's
+    rxq destroy took the whole second, profiles/r5/cross_ctx.jsonl).  The
+    parked buffers, handed to the next rxq of the same size, check frames
+    exactly as fresh ones."""
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    import time
+    from mtcp_amd import gpu
+    from mtcp_amd._lib import lib
+    L, T = lib(), _testing_lib()
+    buf, desc = golden.buf, golden.desc
+    base = buf.ctypes.data
+    part = desc[:512]
+    want = oracle.rx_chunk(buf, part, 0)
+
+    def check(ctx):
+        q = ctypes.c_void_p()
+        assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 512, 512 * 2048) == 0
+        for d in part:
+            assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
+        n = ctypes.c_uint32()
+        assert L.mtcp_gpu_rxq_flush(q, ctypes.byref(n)) == 0 and n.value == len(part)
+        for i in range(len(part)):
+            res = ctypes.c_void_p()
+            L.mtcp_gpu_rxq_get(q, i, None, ctypes.byref(res))
+            got = np.frombuffer(ctypes.string_at(res.value, 40), dtype=RESULT_DTYPE)[0]
+            if want["verdict"][i] != V_BAD_DESC:
+                assert got.tobytes() == want[i].tobytes(), i
+        return q
+
+    a = gpu.Context(0)
+    try:
+        with gpu.Context(0) as first:                        # park one rxq's buffers
+            L.mtcp_gpu_rxq_destroy(check(first))
+        assert T.mtcp_gpu_debug_stall(a._h, 1_000_000) == 0
+        t0 = time.monotonic()
+        b = gpu.Context(0)
+        q = check(b)                                         # the parked buffers, reused
+        L.mtcp_gpu_rxq_destroy(q)
+        b.close()
+        c = gpu.Context(0)
+        c.reserve(1 << 20, 1024)
+        c.close()
+        dt = time.monotonic() - t0
+        assert dt < 0.5, dt                                  # not A's 1 s
+        t1 = time.monotonic()
+        assert L.mtcp_gpu_sync(a._h) == 0
+        assert time.monotonic() - t1 > 0.3                   # A's work was still running
+    finally:
+        a.close()
