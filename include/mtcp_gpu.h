@@ -428,7 +428,12 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues,
                               uint32_t *n_found);
 
 /* Pin / unpin host memory for DMA and zero-copy device access
- * (hipHostRegister; the pattern SURVEY §7 names for DPDK mempools). */
+ * (hipHostRegister; the pattern SURVEY §7 names for DPDK mempools).
+ * Unregistering waits for the work of every stream on the device, other
+ * threads' included (hipHostUnregister; profiles/r5/free_sync.jsonl):
+ * unpin at shutdown, after every context on the device is closed, not on a
+ * thread's own way out.  The library's own buffers are never freed that way
+ * (mtcp_amd/csrc/park.hpp). */
 int mtcp_gpu_host_register(void *ptr, uint64_t len);
 int mtcp_gpu_host_unregister(void *ptr);
 
