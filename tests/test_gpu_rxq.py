@@ -335,3 +335,55 @@ def test_a_shutdown_does_not_wait_for_another_contexts_work(golden):
         assert time.monotonic() - t1 > 0.3                   # A's work was still running
     finally:
         a.close()
+
+
+@pytest.mark.gpu
+def test_parked_buffers_under_concurrent_threads(golden):
+    """Four threads (as four mTCP threads on one GPU) each open a context,
+    create an rxq of one of two sizes, check 256 frames, destroy the rxq and
+    close the context, 12 times over: the parked buffers (park.hpp) move
+    between threads and contexts under its lock, and every batch's records
+    are the oracle's, whichever thread's buffers it got."""
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    import threading
+    from mtcp_amd import gpu
+    from mtcp_amd._lib import lib
+    L = lib()
+    buf, desc = golden.buf, golden.desc
+    base = buf.ctypes.data
+    errors = []
+
+    def worker(t):
+        try:
+            for it in range(12):
+                first = (t * 12 + it) * 97 % (len(desc) - 256)
+                part = desc[first:first + 256]
+                want = oracle.rx_chunk(buf, part, 0)
+                cap = 256 if (t + it) % 2 else 512
+                with gpu.Context(0) as ctx:
+                    q = ctypes.c_void_p()
+                    assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, cap, cap * 2048) == 0
+                    try:
+                        for d in part:
+                            assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
+                        n = ctypes.c_uint32()
+                        assert L.mtcp_gpu_rxq_flush(q, ctypes.byref(n)) == 0 and n.value == 256
+                        for i in range(256):
+                            res = ctypes.c_void_p()
+                            L.mtcp_gpu_rxq_get(q, i, None, ctypes.byref(res))
+                            got = np.frombuffer(ctypes.string_at(res.value, 40), dtype=RESULT_DTYPE)[0]
+                            if want["verdict"][i] != V_BAD_DESC:
+                                assert got.tobytes() == want[i].tobytes(), (t, it, i)
+                    finally:
+                        L.mtcp_gpu_rxq_destroy(q)
+        except Exception as e:                     # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not any(th.is_alive() for th in threads)
+    assert not errors, errors[:3]
