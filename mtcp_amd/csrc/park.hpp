@@ -15,9 +15,10 @@
 // the next thread's (or the next context's) buffer.
 //
 // Bounds: buffers above kParkMaxBytes (a bench-sized reserve) are freed as
-// before, and at most kParkDeviceBytes are parked per device (past that a
-// release frees).  The caller has made the buffer's device current and has
-// finished its own work on the buffer (its streams are synchronised).
+// before, and at most kParkDeviceBytes of each kind (pinned host, device)
+// are parked per device (past that a release frees).  The caller has made
+// the buffer's device current and has finished its own work on the buffer
+// (its streams are synchronised).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
