@@ -280,15 +280,18 @@ def test_rxq_passes_its_size_hint(size, kernel):
 
 @pytest.mark.gpu
 def test_a_shutdown_does_not_wait_for_another_contexts_work(golden):
-    """Two mTCP threads on one GPU: thread A's context has 1 s of work queued
-    (mtcp_gpu_debug_stall), thread B creates an rxq, checks a batch, destroys
-    the rxq, closes its context, and a third thread opens and reserves one.
-    None of B's or C's calls waits for A: the library parks its buffers
+    """Two mTCP threads on one GPU: thread B has checked a batch through its
+    rxq when thread A's context gets 1 s of work queued
+    (mtcp_gpu_debug_stall); B then destroys its rxq and closes its context.
+    Neither release waits for A: the library parks its buffers
     (mtcp_amd/csrc/park.hpp) instead of hipFree / hipHostFree, which wait for
     every stream on the device (tools/free_sync_probe.py; before parking B's
-    rxq destroy took the whole second, profiles/r5/cross_ctx.jsonl).  The
-    parked buffers, handed to the next rxq of the same size, check frames
-    exactly as fresh ones."""
+    rxq destroy took the whole second, profiles/r5/cross_ctx.jsonl).  Once A
+    is done, a fresh context's rxq of the same size gets B's parked buffers
+    and checks frames exactly as fresh ones.  (Only the releases are timed:
+    new work of B's could share a hardware queue with A's stall once the
+    process has more streams than GPU_MAX_HW_QUEUES, e.g. after the
+    abandoned contexts earlier tests leave, and wait behind it.)"""
     if not torch.cuda.is_available():
         pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
     import time
@@ -317,22 +320,20 @@ def test_a_shutdown_does_not_wait_for_another_contexts_work(golden):
 
     a = gpu.Context(0)
     try:
-        with gpu.Context(0) as first:                        # park one rxq's buffers
-            L.mtcp_gpu_rxq_destroy(check(first))
+        b = gpu.Context(0)
+        q = check(b)
         assert T.mtcp_gpu_debug_stall(a._h, 1_000_000) == 0
         t0 = time.monotonic()
-        b = gpu.Context(0)
-        q = check(b)                                         # the parked buffers, reused
         L.mtcp_gpu_rxq_destroy(q)
         b.close()
-        c = gpu.Context(0)
-        c.reserve(1 << 20, 1024)
-        c.close()
         dt = time.monotonic() - t0
-        assert dt < 0.5, dt                                  # not A's 1 s
         t1 = time.monotonic()
         assert L.mtcp_gpu_sync(a._h) == 0
-        assert time.monotonic() - t1 > 0.3                   # A's work was still running
+        a_left = time.monotonic() - t1
+        assert dt < 0.3, dt                                  # not A's 1 s
+        assert a_left > 0.5, a_left                          # A's work was still running
+        with gpu.Context(0) as d:                            # B's parked buffers, reused
+            L.mtcp_gpu_rxq_destroy(check(d))
     finally:
         a.close()
 
@@ -360,10 +361,10 @@ def test_parked_buffers_under_concurrent_threads(golden):
                 first = (t * 12 + it) * 97 % (len(desc) - 256)
                 part = desc[first:first + 256]
                 want = oracle.rx_chunk(buf, part, 0)
-                cap = 256 if (t + it) % 2 else 512
+                cap = 256 if (t + it) % 2 else 512           # frames; golden frames reach 16 000 B
                 with gpu.Context(0) as ctx:
                     q = ctypes.c_void_p()
-                    assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, cap, cap * 2048) == 0
+                    assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, cap, cap * 65536) == 0
                     try:
                         for d in part:
                             assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0

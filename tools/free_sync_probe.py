@@ -82,6 +82,28 @@ def main():
     timed("hipHostUnregister", registered, lambda p: H.hipHostUnregister(p))
     timed("hipStreamDestroy", stream, lambda t: H.hipStreamDestroy(t))
     timed("hipEventDestroy", event, lambda e: H.hipEventDestroy(e))
+    H.hipMemcpy.argtypes = [vp, vp, sz, ctypes.c_int]
+    H.hipMemcpyAsync.argtypes = [vp, vp, sz, ctypes.c_int, vp]
+    H.hipGetDeviceProperties = getattr(H, "hipGetDevicePropertiesR0600", H.hipGetDeviceProperties)
+    H.hipGetDeviceProperties.argtypes = [vp, ctypes.c_int]
+    small = ctypes.create_string_buffer(4096)
+    timed("hipStreamCreateWithFlags", lambda: None, lambda _: H.hipStreamCreateWithFlags(ctypes.byref(vp()), 1))
+    timed("hipEventCreateWithFlags", lambda: None, lambda _: H.hipEventCreateWithFlags(ctypes.byref(vp()), 2))
+    timed("hipGetDeviceProperties", lambda: None,
+          lambda _: H.hipGetDeviceProperties(ctypes.cast(ctypes.create_string_buffer(8192), vp), 0))
+    timed("hipMemcpy H2D 4 KiB pageable (null stream)", dmalloc,
+          lambda p: H.hipMemcpy(p, ctypes.cast(small, vp), 4096, 1))
+    timed("hipMemcpyAsync H2D 4 KiB + own stream sync", dmalloc,
+          lambda p: H.hipMemcpyAsync(p, ctypes.cast(small, vp), 4096, 1, s) or H.hipStreamSynchronize(s))
+    from mtcp_amd import gpu as _g
+    timed("mtcp_gpu_open", lambda: None, lambda _: _g.Context(0) and 0)
+    def ctx_prep():
+        return _g.Context(0)
+    timed("mtcp_gpu_reserve(1 MiB, 1024)", ctx_prep, lambda c: c.reserve(1 << 20, 1024) or 0)
+    def rxq_make(c):
+        q = vp()
+        return L.mtcp_gpu_rxq_create(ctypes.byref(q), c._h, 256, 256 * 2048)
+    timed("mtcp_gpu_rxq_create(256, 512 KiB)", ctx_prep, rxq_make)
     timed("hipMalloc", lambda: None, lambda _: H.hipMalloc(ctypes.byref(vp()), n))
     timed("hipHostMalloc", lambda: None, lambda _: H.hipHostMalloc(ctypes.byref(vp()), n, 0))
     a.close()
