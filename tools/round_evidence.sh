@@ -33,4 +33,7 @@ bash tools/gpu_steps.sh \
   "txsw|120|MTCP_GPU_TX=0 oracle/_ref/dropin_tx /tmp/txsw.bin 4096 observe && MTCP_GPU_TX=1 oracle/_ref/dropin_tx /tmp/txgpu.bin 4096 observe && cmp /tmp/txhang.bin /tmp/txsw.bin && cmp /tmp/txgpu.bin /tmp/txsw.bin && echo tx-frames-identical" \
   "dmap|400|OUT=gpurun_out/dispatch_map.jsonl bash tools/dispatch_map.sh" \
   "pr|240|bash tools/profile_rows.sh gpurun_out/prof_rows" \
+  "xctx|120|python -u tools/cross_ctx_probe.py > gpurun_out/cross_ctx.json" \
+  "free|120|python -u tools/free_sync_probe.py > gpurun_out/free_sync.jsonl" \
+  "stop|120|MTCP_GPU_PIPELINE=1 MTCP_GPU_TX=0 MTCP_GPU_WAIT_TIMEOUT_MS=100 MTCP_GPU_STALL_AFTER=1 MTCP_GPU_STALL_US=1500000 oracle/_ref/dropin_rx tests/golden/rx_buf.bin tests/golden/rx_desc.bin /tmp/stop.bin observe stop > gpurun_out/shutdown_inflight.json" \
   "wp|120|./tools/wave_probe 1500 64 1024 4096 16384 32768 && ./tools/wave_probe 9000 64 4096 16384 && ./tools/wave_probe 64 64 4096 16384 65536"
