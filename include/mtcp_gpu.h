@@ -57,8 +57,19 @@
  * the verdict only); results belong to the caller.
  *
  * Threading: one context per mTCP thread (mtcp/src/core.c:1057 pins one
- * thread per core); a context owns one HIP stream and its staging buffers and
- * is not re-entrant.  Distinct contexts may be used concurrently.
+ * thread per core); a context owns one HIP stream (mtcp_gpu_stream) and its
+ * staging buffers and is not re-entrant.  Distinct contexts may be used
+ * concurrently.  Everything a context does runs on that one stream — its
+ * device-resident launches with stream NULL, its host-memory calls, its
+ * rxqs' flushes (mtcp_gpu_rxq.h) — except a host-memory rx call over more
+ * than 64 MiB, which pipelines through two more streams of its own.  HIP
+ * maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues per device
+ * (4 by default): up to that many contexts on one device never share a
+ * queue, so one context's stalled work cannot hold up another's.
+ *
+ * Waits: mtcp_gpu_set_wait_limit bounds every wait of every synchronous call
+ * on a context (see there).  Without a limit the synchronous calls block
+ * until the GPU is done, as hipStreamSynchronize does.
  */
 #ifndef MTCP_GPU_H
 #define MTCP_GPU_H
@@ -70,10 +81,13 @@
 extern "C" {
 #endif
 
-#define MTCP_GPU_ABI_VERSION 4   /* 2: MTCP_GPU_F_COMPACT, mtcp_gpu_result16;
+#define MTCP_GPU_ABI_VERSION 5   /* 2: MTCP_GPU_F_COMPACT, mtcp_gpu_result16;
                                     3: mtcp_gpu_rxq_get16, mtcp_gpu_debug_stall moved to the test library;
                                     4: mtcp_gpu_tx_fill_ptrs_for, mtcp_gpu_host_stream,
-                                       mtcp_gpu_size_hint, mtcp_gpu_rx_chunk_hint_dev */
+                                       mtcp_gpu_size_hint, mtcp_gpu_rx_chunk_hint_dev;
+                                    5: mtcp_gpu_set_wait_limit, mtcp_gpu_wait_limit (every
+                                       synchronous call bounded); mtcp_gpu_host_stream removed
+                                       (host calls run on mtcp_gpu_stream) */
 
 /* ---- error codes (negative returns) ----------------------------------- */
 #define MTCP_GPU_OK        0
@@ -216,7 +230,51 @@ int         mtcp_gpu_device_pci_bus_id(int device, char *buf, int len);
  */
 int  mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key,
                    int rss_num_queues, uint32_t flags);
+
+/* Bound of mtcp_gpu_open's one wait (the first context with a given RSS key
+ * on a device uploads the key's tables on its new stream): past it open
+ * answers MTCP_GPU_ETIMEDOUT and returns no context. */
+#define MTCP_GPU_OPEN_WAIT_US 2000000u
+
+/*
+ * Close: the context's own work finishes first (within its wait limit, if
+ * set; past it the context is abandoned as below and close returns without
+ * waiting more).  Work the CALLER queued on its own streams through the
+ * *_dev entry points is not waited for: the device-side RSS tables such a
+ * launch reads are shared by every context with the same key and never
+ * freed, so the launch computes with its own key whatever contexts are
+ * opened or closed meanwhile; every other buffer of it is the caller's, who
+ * must keep it alive until that stream is done.
+ */
 void mtcp_gpu_close(mtcp_gpu_ctx *ctx);
+
+/*
+ * Bound every wait of the context's synchronous calls to timeout_us
+ * (0: no bound, the default).  Each call computes one deadline when it
+ * starts and polls the GPU until then instead of blocking; the calls are
+ * mtcp_gpu_rx_chunk, _rx_ptrs, _tx_fill, _tx_fill_ptrs (whose
+ * _tx_fill_ptrs_for argument, when non-zero, overrides the limit),
+ * _flow_hash, _addr_pool_search, _reserve, _sync and _close, and the calls
+ * of the context's rxqs (mtcp_gpu_rxq.h: create, flush, wait, destroy; an
+ * rxq takes the limit its context has when it is created).
+ *
+ * A call whose GPU work is not done by the deadline answers
+ * MTCP_GPU_ETIMEDOUT and ABANDONS the context: that work may still run, so
+ * every later call on the context answers MTCP_GPU_EIO without touching the
+ * device, and mtcp_gpu_close frees only its host-side state (its streams and
+ * buffers stay allocated, never used again).  Nothing is written into the
+ * caller's memory after such a return, and nothing of it is read: with a
+ * limit, the host calls copy the caller's input into pinned staging first
+ * and the GPU's output back out of pinned staging only once it is complete
+ * (one more host copy of the input, the price of the bound).  The caller
+ * then does the work itself, as mTCP does when dev_ioctl answers -1
+ * (mtcp/src/ip_in.c:29-31, tcp_in.c:1160-1164, ip_out.c:147-165,
+ * tcp_out.c:320-329).  mtcp_gpu_sync alone does not abandon: it answers
+ * MTCP_GPU_ETIMEDOUT and the context stays usable (what it waits for is the
+ * caller's own device work).
+ */
+int      mtcp_gpu_set_wait_limit(mtcp_gpu_ctx *ctx, uint32_t timeout_us);
+uint32_t mtcp_gpu_wait_limit(const mtcp_gpu_ctx *ctx);
 
 /*
  * Optional, at init time (an io_module's init_handle): allocate the device
@@ -232,13 +290,12 @@ int  mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts);
 /* dev_ioctl-compatible capability answer (0 = offloaded, -1 = software). */
 int  mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp);
 
-/* The HIP stream the context launches on (a hipStream_t, as void*). */
+/* The HIP stream the context runs on (a hipStream_t, as void*): its
+ * device-resident launches with stream NULL, its host-memory calls and its
+ * rxqs.  A caller may order its own work after the context's on it; work it
+ * queues there runs before the context's next calls and counts against their
+ * wait limit. */
 void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx);
-
-/* The HIP stream the host-memory calls (mtcp_gpu_rx_chunk's first stage,
- * _rx_ptrs, _tx_fill, _tx_fill_ptrs[_for], _flow_hash) run on, created on
- * first use; NULL if it cannot be created or the context was abandoned. */
-void *mtcp_gpu_host_stream(mtcp_gpu_ctx *ctx);
 
 /* Bytes per rx result record this context writes: 40, or 16 with
  * MTCP_GPU_F_COMPACT; 0 for a NULL context. */
@@ -311,11 +368,12 @@ int mtcp_gpu_rx_chunk_hint_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t bu
 
 /*
  * Host-memory rx (the drop-in for the rx loop): chunk and descriptors in host
- * memory, results written to host memory; synchronous.  Large chunks are
- * streamed H2D -> kernel -> D2H through pinned staging on several streams;
- * register the chunk with mtcp_gpu_host_register for full PCIe rate.
- * Descriptor offsets must be non-decreasing for the streamed path (PSIO
- * chunks are); otherwise the chunk is staged whole.
+ * memory, results written to host memory; synchronous, bounded by the
+ * context's wait limit.  Large chunks are streamed H2D -> kernel -> D2H in
+ * 64 MiB stages on up to three streams; register the chunk with
+ * mtcp_gpu_host_register for full PCIe rate (without a wait limit the DMA
+ * reads it in place).  Descriptor offsets must be non-decreasing for the
+ * streamed path (PSIO chunks are); otherwise the chunk is staged whole.
  */
 int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
                       const mtcp_gpu_desc *desc, uint32_t n, uint32_t off_shift,
@@ -333,7 +391,9 @@ int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts,
  *   tcph->check = TCPCalcChecksum(tcph, tot_len - 4*ihl, saddr, daddr)
  *                                             computed with check = 0
  * Other frames are left untouched.  *n_filled (may be NULL) receives the
- * number of frames written (host variant only).
+ * number of frames written (host variant only).  The host variant sends the
+ * chunk to the GPU once and gets back 8 B per frame (the two check values):
+ * only the check fields of the chunk are written, by the calling thread.
  */
 int mtcp_gpu_tx_fill_dev(mtcp_gpu_ctx *ctx, void *d_buf, uint64_t buf_len,
                          const mtcp_gpu_desc *d_desc, uint32_t n,
@@ -357,16 +417,14 @@ int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_
                           uint32_t n, uint32_t *n_filled);
 
 /*
- * mtcp_gpu_tx_fill_ptrs with a bound on the wait (timeout_us 0: none, exactly
- * mtcp_gpu_tx_fill_ptrs).  If the GPU has not reported within timeout_us,
- * nothing has been written into the caller's frames, MTCP_GPU_ETIMEDOUT is
- * returned, and the context is ABANDONED: the copies it gave up on may still
- * run into its staging, so every later call on it answers MTCP_GPU_EIO
- * without touching the device, and mtcp_gpu_close frees only its host-side
- * state (its streams and buffers stay allocated).  The caller fills the
- * frames itself, as mTCP does when dev_ioctl answers -1 (tcp_out.c:320-329,
- * ip_out.c:147-165): an io_module's send_pkts (core.c:818-824) never blocks
- * on a GPU that stopped answering.
+ * mtcp_gpu_tx_fill_ptrs with its own bound on the wait (timeout_us 0: the
+ * context's wait limit, i.e. exactly mtcp_gpu_tx_fill_ptrs).  If the GPU has
+ * not reported within the bound, nothing has been written into the caller's
+ * frames, MTCP_GPU_ETIMEDOUT is returned and the context is ABANDONED
+ * (mtcp_gpu_set_wait_limit).  The caller fills the frames itself, as mTCP
+ * does when dev_ioctl answers -1 (tcp_out.c:320-329, ip_out.c:147-165): an
+ * io_module's send_pkts (core.c:818-824) never blocks on a GPU that stopped
+ * answering.
  */
 int mtcp_gpu_tx_fill_ptrs_for(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_t *lens,
                               uint32_t n, uint32_t *n_filled, uint32_t timeout_us);
@@ -437,7 +495,8 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues,
 int mtcp_gpu_host_register(void *ptr, uint64_t len);
 int mtcp_gpu_host_unregister(void *ptr);
 
-/* Synchronise the context's stream. */
+/* Synchronise the context's stream (within its wait limit, if set:
+ * MTCP_GPU_ETIMEDOUT past it, the context still usable). */
 int mtcp_gpu_sync(mtcp_gpu_ctx *ctx);
 
 /* (The fault-injection entry point the hang tests use, mtcp_gpu_debug_stall,

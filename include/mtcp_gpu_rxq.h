@@ -28,7 +28,9 @@
  *
  * An rxq's copies and kernel run on its context's stream (mtcp_gpu_stream),
  * with its own completion event; one context per mTCP thread, its rxqs used
- * by that thread only (not re-entrant).
+ * by that thread only (not re-entrant).  Every wait of an rxq (create's,
+ * flush's, wait's, destroy's) is bounded by the wait limit its context had
+ * when the rxq was created (mtcp_gpu_set_wait_limit; none by default).
  */
 #ifndef MTCP_GPU_RXQ_H
 #define MTCP_GPU_RXQ_H
@@ -49,7 +51,8 @@ typedef struct mtcp_gpu_rxq mtcp_gpu_rxq;
 int  mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts,
                          uint64_t max_bytes);
 
-/* Free the rxq.  A flush still in flight is waited for.  After
+/* Free the rxq.  A flush still in flight is waited for (within the wait
+ * limit; past it the buffers are left allocated, as below).  After
  * mtcp_gpu_rxq_wait_for gave up on a flush (MTCP_GPU_ETIMEDOUT), that flush
  * may still copy into the staging and results: destroy then waits for it at
  * most MTCP_GPU_RXQ_DESTROY_WAIT_US more, and if it still has not finished,
@@ -84,7 +87,8 @@ int  mtcp_gpu_rxq_flush(mtcp_gpu_rxq *q, uint32_t *n);
 int  mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q);
 int  mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n);
 
-/* rxq_wait with a limit (timeout_us 0: none).  If the results are not in
+/* rxq_wait with a limit (timeout_us 0: the context's wait limit,
+ * mtcp_gpu_set_wait_limit, i.e. exactly rxq_wait).  If the results are not in
  * after timeout_us, the flush is abandoned and MTCP_GPU_ETIMEDOUT returned:
  * its frames stay staged (served by rxq_frame, without verdicts), the rxq
  * takes resets and pushes again, but no further flush (MTCP_GPU_EIO: the

@@ -15,7 +15,8 @@ LIB_PATH = os.path.join(HERE, "lib", "libmtcp_gpu.so")
 EXPORTS = (
     "mtcp_gpu_abi_version", "mtcp_gpu_strerror", "mtcp_gpu_device_count", "mtcp_gpu_device_pci_bus_id",
     "mtcp_gpu_open",
-    "mtcp_gpu_close", "mtcp_gpu_reserve", "mtcp_gpu_dev_ioctl", "mtcp_gpu_stream", "mtcp_gpu_host_stream",
+    "mtcp_gpu_close", "mtcp_gpu_reserve", "mtcp_gpu_dev_ioctl", "mtcp_gpu_stream", "mtcp_gpu_set_wait_limit",
+    "mtcp_gpu_wait_limit",
     "mtcp_gpu_record_size", "mtcp_gpu_last_kernel", "mtcp_gpu_rx_chunk_dev",
     "mtcp_gpu_rx_ptrs_dev", "mtcp_gpu_rx_chunk", "mtcp_gpu_rx_ptrs", "mtcp_gpu_tx_fill_dev",
     "mtcp_gpu_tx_fill", "mtcp_gpu_rx_chunk_flow_dev", "mtcp_gpu_rx_ptrs_flow_dev", "mtcp_gpu_rx_chunk_hint_dev",
@@ -58,7 +59,8 @@ def lib() -> ctypes.CDLL:
         "mtcp_gpu_reserve": ([vp, u64, u32], i32),
         "mtcp_gpu_dev_ioctl": ([vp, i32, i32, vp], i32),
         "mtcp_gpu_stream": ([vp], vp),
-        "mtcp_gpu_host_stream": ([vp], vp),
+        "mtcp_gpu_set_wait_limit": ([vp, u32], i32),
+        "mtcp_gpu_wait_limit": ([vp], u32),
         "mtcp_gpu_record_size": ([vp], u32),
         "mtcp_gpu_last_kernel": ([vp], ctypes.c_char_p),
         "mtcp_gpu_sync": ([vp], i32),

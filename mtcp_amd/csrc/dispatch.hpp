@@ -116,8 +116,10 @@ inline int pick_sched(int forced, uint32_t n, uint64_t slot, bool small_only, bo
             // kernel's 4.82; an IMIX of 4 K frames keeps the wave kernel,
             // 3.86 against 5.06: profiles/r5/dispatch_map.jsonl)
             s = kSchedOct;
-        } else if (narrow && slot <= 320 && n <= (1u << 17)) {
+        } else if (narrow && slot <= 320 && n > 2048 && n <= (1u << 17)) {
             // 128 K frames of 256 B: quads, 8.55 against the span kernel's 9.27 us
+            // (a hinted batch of <= 2 048 frames keeps the wave kernel, as an
+            // unhinted one: the map has no measured quad cell below 4 K frames)
             s = kSchedQuad;
         } else if (slot >= 4096) {
             s = n <= (1u << 16) || (narrow && slot <= kWaveNarrowUpToSlot && n >= kWaveNarrowFromPkts)

@@ -12,8 +12,9 @@
 #include <string.h>
 
 #include <algorithm>
-#include <chrono>
+#include <mutex>
 #include <new>
+#include <vector>
 
 #include "../../include/mtcp_gpu.h"
 #include "dispatch.hpp"
@@ -22,6 +23,7 @@
 #include "park.hpp"
 #include "rx_kernels.hpp"
 #include "rx_span.hpp"
+#include "wait.hpp"
 
 namespace {
 
@@ -29,6 +31,11 @@ constexpr int kStages = 3;                       // H2D | kernel | D2H overlap
 constexpr uint64_t kStageBytes = 64ull << 20;    // chunk bytes per pipeline stage
 constexpr uint32_t kStagePkts = 1u << 16;        // descriptors per pipeline stage
 
+// One pipeline stage of the host-memory calls.  Stage 0 runs on the
+// context's own stream (one stream per mTCP thread: an io_module's rxqs, its
+// tx fills and every host call of a batch that fits one stage share it);
+// stages 1 and 2 get streams of their own only when a call spans more than
+// one stage (a chunk above kStageBytes), to overlap H2D, kernel and D2H.
 struct Stage {
     uint8_t *d_buf = nullptr;
     mtcp_gpu_desc *d_desc = nullptr;
@@ -36,7 +43,18 @@ struct Stage {
     uint64_t buf_cap = 0;
     uint32_t pkt_cap = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = false;
+    // bounded calls (a context wait limit): pinned bounce buffers, so that
+    // no copy the call gives up on can read or write the caller's memory
+    uint8_t *h_in = nullptr;                    // caller data -> H2D
+    uint64_t h_in_cap = 0;
+    uint8_t *h_out = nullptr;                   // D2H -> caller data
+    uint64_t h_out_cap = 0;
+    uint32_t pend_first = 0, pend_cnt = 0;      // records of this stage's batch not yet copied out
 };
+
+using mtcp_wait::Deadline;
+using mtcp_wait::drain;
 
 }  // namespace
 
@@ -49,18 +67,17 @@ struct mtcp_gpu_ctx {
     uint32_t rss_key_w[4] = {0, 0, 0, 0};        // key bytes 0..15, big-endian words
     int sched = 0;                               // Sched: kSchedAuto unless MTCP_GPU_SCHED forces one
     hipStream_t stream = nullptr;
-    uint32_t *d_rss_tables = nullptr;
-    uint32_t *d_count = nullptr;
+    const uint32_t *d_rss_tables = nullptr;      // shared, immutable (rss_tables_for)
+    uint32_t wait_us = 0;                        // mtcp_gpu_set_wait_limit (0: no limit)
     Stage stage[kStages];
     uint8_t *h_gather = nullptr;                 // pinned, for rx_ptrs
     uint64_t h_gather_cap = 0;
     mtcp_gpu_desc *h_gather_desc = nullptr;
     uint32_t h_gather_desc_cap = 0;
     const char *last_kernel = "";                // mtcp_gpu_last_kernel
-    hipEvent_t done_evt = nullptr;               // completion of a bounded host call
-    // a host call's bounded wait gave up (mtcp_gpu_tx_fill_ptrs_for): work of
-    // that call may still read or write the staging, so nothing is issued,
-    // staged or freed on this context again (every call answers EIO)
+    // a host call's bounded wait gave up: work of that call may still read
+    // or write the staging, so nothing is issued, staged or freed on this
+    // context again (every call answers EIO)
     bool abandoned = false;
 };
 
@@ -301,18 +318,42 @@ void stage_release_pkts(Stage &s) {
     s.d_out = nullptr;
     s.pkt_cap = 0;
 }
+void stage_release_host(Stage &s) {
+    mtcp_park::release(s.h_in, s.h_in_cap, mtcp_park::kHost);
+    mtcp_park::release(s.h_out, s.h_out_cap, mtcp_park::kHost);
+    s.h_in = s.h_out = nullptr;
+    s.h_in_cap = s.h_out_cap = 0;
+}
 
-int stage_reserve(mtcp_gpu_ctx *ctx, Stage &s, uint64_t bytes, uint32_t pkts) {
+// A wait of a host call ended: past the deadline the context is abandoned
+// (the work it gave up on may still use the staging), and the call answers
+// MTCP_GPU_ETIMEDOUT.
+int waited(mtcp_gpu_ctx *ctx, int rc) {
+    if (rc == MTCP_GPU_ETIMEDOUT) ctx->abandoned = true;
+    return rc;
+}
+
+// The stage's stream: stage 0 is the context's own; the others are created
+// on the first call that spans more than one stage.
+int stage_stream(mtcp_gpu_ctx *ctx, Stage &s) {
+    if (s.stream) return MTCP_GPU_OK;
+    if (&s == &ctx->stage[0]) {
+        s.stream = ctx->stream;
+        return MTCP_GPU_OK;
+    }
+    if (!HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking))) return MTCP_GPU_EIO;
+    s.own_stream = true;
+    return MTCP_GPU_OK;
+}
+
+int stage_reserve(mtcp_gpu_ctx *ctx, Stage &s, uint64_t bytes, uint32_t pkts, const Deadline &dl) {
     if (ctx->abandoned) return MTCP_GPU_EIO;
-    // a stage's stream exists once a host call uses the stage (a context
-    // that only launches device-resident work, or serves an io_module's
-    // rxqs, has the one stream of mtcp_gpu_open)
-    if (!s.stream && !HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)))
-        return MTCP_GPU_EIO;
+    int rc = stage_stream(ctx, s);
+    if (rc != MTCP_GPU_OK) return rc;
     // growing releases buffers that the stage's previous batch may still
     // use: drain that batch first (park.hpp releases without any device wait)
-    if ((bytes > s.buf_cap || pkts > s.pkt_cap) && s.stream && !HIP_OK(hipStreamSynchronize(s.stream)))
-        return MTCP_GPU_EIO;
+    if ((bytes > s.buf_cap || pkts > s.pkt_cap) && (rc = waited(ctx, drain(s.stream, dl))) != MTCP_GPU_OK)
+        return rc;
     if (bytes > s.buf_cap) {
         stage_release_buf(s);
         const uint64_t cap = (bytes + 4095) & ~4095ull;
@@ -330,6 +371,135 @@ int stage_reserve(mtcp_gpu_ctx *ctx, Stage &s, uint64_t bytes, uint32_t pkts) {
         }
         s.pkt_cap = pkts;
     }
+    return MTCP_GPU_OK;
+}
+
+// Pinned host buffers of a stage: in_bytes of bounce for the caller's input
+// (a bounded call copies it there first), out_bytes for what comes back.
+// The stage's stream has no work on them (a grown buffer is released).
+int stage_host(mtcp_gpu_ctx *ctx, Stage &s, uint64_t in_bytes, uint64_t out_bytes, const Deadline &dl) {
+    int rc = MTCP_GPU_OK;
+    if ((in_bytes > s.h_in_cap || out_bytes > s.h_out_cap) && s.stream &&
+        (rc = waited(ctx, drain(s.stream, dl))) != MTCP_GPU_OK)
+        return rc;
+    if (in_bytes > s.h_in_cap) {
+        mtcp_park::release(s.h_in, s.h_in_cap, mtcp_park::kHost);
+        s.h_in = nullptr;
+        s.h_in_cap = 0;
+        const uint64_t cap = (in_bytes + 4095) & ~4095ull;
+        if (!HIP_OK(mtcp_park::alloc(&s.h_in, cap, mtcp_park::kHost))) return MTCP_GPU_ENOMEM;
+        s.h_in_cap = cap;
+    }
+    if (out_bytes > s.h_out_cap) {
+        mtcp_park::release(s.h_out, s.h_out_cap, mtcp_park::kHost);
+        s.h_out = nullptr;
+        s.h_out_cap = 0;
+        const uint64_t cap = (out_bytes + 4095) & ~4095ull;
+        if (!HIP_OK(mtcp_park::alloc(&s.h_out, cap, mtcp_park::kHost))) return MTCP_GPU_ENOMEM;
+        s.h_out_cap = cap;
+    }
+    return MTCP_GPU_OK;
+}
+
+// A bounded call's copy of caller memory into a bounce buffer (16 B aligned
+// destination; streaming stores: the DMA engine reads it next, not a core)
+void bounce_in(uint8_t *dst, const void *src, uint64_t len) {
+    const uint8_t *p = static_cast<const uint8_t *>(src);
+    constexpr uint64_t kPiece = 1u << 30;
+    for (uint64_t o = 0; o < len; o += kPiece)
+        stage_copy(dst + o, p + o, (uint32_t)std::min(kPiece, len - o));
+    stage_fence();
+}
+
+// The end of a host call that used stages [0, nstages): every stage's
+// stream drained within the call's deadline, the records of a bounded
+// call's batches still in the stages' bounce buffers copied out to `out_b`
+// (rec bytes each).  Returns the call's result: rc if every drain
+// succeeded, MTCP_GPU_ETIMEDOUT (the context abandoned, nothing more copied
+// out) past the deadline.
+int finish_call(mtcp_gpu_ctx *ctx, int rc, const Deadline &dl, int nstages, uint8_t *out_b = nullptr,
+                size_t rec = 0) {
+    for (int i = 0; i < nstages; ++i) {
+        Stage &s = ctx->stage[i];
+        if (!s.stream) continue;
+        const int r = drain(s.stream, dl);
+        if (r == MTCP_GPU_ETIMEDOUT) {
+            for (auto &t : ctx->stage) t.pend_cnt = 0;
+            return waited(ctx, r);
+        }
+        if (r != MTCP_GPU_OK && rc == MTCP_GPU_OK) rc = r;
+    }
+    for (int i = 0; i < nstages; ++i) {
+        Stage &s = ctx->stage[i];
+        if (rc == MTCP_GPU_OK && s.pend_cnt && out_b)
+            memcpy(out_b + (size_t)s.pend_first * rec, s.h_out, (size_t)s.pend_cnt * rec);
+        s.pend_cnt = 0;
+    }
+    return rc;
+}
+
+// A bounded call reuses stage s for its next batch: the batch it holds
+// finishes (within the deadline) and its records are copied out.
+int stage_collect(mtcp_gpu_ctx *ctx, Stage &s, uint8_t *out_b, size_t rec, const Deadline &dl) {
+    if (!s.pend_cnt) return MTCP_GPU_OK;
+    const int rc = waited(ctx, drain(s.stream, dl));
+    if (rc != MTCP_GPU_OK) return rc;
+    memcpy(out_b + (size_t)s.pend_first * rec, s.h_out, (size_t)s.pend_cnt * rec);
+    s.pend_cnt = 0;
+    return MTCP_GPU_OK;
+}
+
+// The Toeplitz tables of one RSS key on one device (build_rss_tables):
+// built and uploaded by the first context opened with that key, then shared
+// by every later one, never written again and never freed.  So a kernel
+// still reading them — a *_dev launch on a caller's stream that has not
+// finished when its context is closed — reads the key it was launched with,
+// whatever contexts open or close meanwhile.  At most one set of 1.5 KiB
+// per distinct key and device.
+struct RssTables {
+    int device;
+    uint8_t key[40];
+    uint32_t host[mg::kRssTableWords];           // the upload's source, kept with the tables
+    uint32_t *d;
+};
+
+std::mutex &rss_mutex() {
+    static std::mutex *m = new std::mutex;
+    return *m;
+}
+std::vector<RssTables *> &rss_cache() {
+    static std::vector<RssTables *> *v = new std::vector<RssTables *>;
+    return *v;
+}
+
+// Bound of the one wait at mtcp_gpu_open (a new key's table upload on the
+// new context's stream), before any limit can be set on the context.
+constexpr uint32_t kOpenWaitUs = 2000000;
+
+int rss_tables_for(int device, const uint8_t key[40], hipStream_t st, const uint32_t **out) {
+    {
+        std::lock_guard<std::mutex> lk(rss_mutex());
+        for (const RssTables *t : rss_cache())
+            if (t->device == device && memcmp(t->key, key, 40) == 0) {
+                *out = t->d;
+                return MTCP_GPU_OK;
+            }
+    }
+    RssTables *t = new (std::nothrow) RssTables;
+    if (!t) return MTCP_GPU_ENOMEM;
+    t->device = device;
+    memcpy(t->key, key, 40);
+    build_rss_tables(key, t->host);
+    if (!HIP_OK(hipMalloc(&t->d, sizeof(t->host)))) {
+        delete t;
+        return MTCP_GPU_ENOMEM;
+    }
+    int rc = HIP_OK(hipMemcpyAsync(t->d, t->host, sizeof(t->host), hipMemcpyHostToDevice, st))
+                 ? drain(st, Deadline(kOpenWaitUs)) : MTCP_GPU_EIO;
+    if (rc != MTCP_GPU_OK) return rc;            // t and its buffer stay (the copy may still run)
+    std::lock_guard<std::mutex> lk(rss_mutex());
+    rss_cache().push_back(t);
+    *out = t->d;
     return MTCP_GPU_OK;
 }
 
@@ -403,63 +573,81 @@ int mtcp_gpu_open(mtcp_gpu_ctx **out, int device, const uint8_t *rss_key, int rs
     if (HIP_OK(hipGetDeviceProperties(&prop, device)) && prop.multiProcessorCount > 0)
         ctx->num_cu = prop.multiProcessorCount;
 
-    uint32_t tables[mg::kRssTableWords];
     const uint8_t *key = rss_key ? rss_key : key05;
-    build_rss_tables(key, tables);
     for (int i = 0; i < 4; ++i)
         ctx->rss_key_w[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) |
                             ((uint32_t)key[4 * i + 2] << 8) | (uint32_t)key[4 * i + 3];
     ctx->sched = sched_from_env();
-    int rc = MTCP_GPU_OK;
-    if (!HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) ||
-        !HIP_OK(mtcp_park::alloc(&ctx->d_rss_tables, sizeof(tables), mtcp_park::kDevice)) ||
-        !HIP_OK(mtcp_park::alloc(&ctx->d_count, sizeof(uint32_t), mtcp_park::kDevice)) ||
-        !HIP_OK(hipMemcpy(ctx->d_rss_tables, tables, sizeof(tables), hipMemcpyHostToDevice)))
-        rc = MTCP_GPU_ENOMEM;
+    // one stream per context: its device-resident launches, the host calls
+    // that fit one stage and its rxqs all go on it (the context's tables are
+    // uploaded on it too, never through the null stream)
+    int rc = HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) ? MTCP_GPU_OK : MTCP_GPU_ENOMEM;
+    if (rc == MTCP_GPU_OK) rc = rss_tables_for(device, key, ctx->stream, &ctx->d_rss_tables);
+    if (rc == MTCP_GPU_ETIMEDOUT) {
+        ctx->abandoned = true;                   // the upload may still run: leave the stream
+        delete ctx;
+        return rc;
+    }
     if (rc != MTCP_GPU_OK) {
         mtcp_gpu_close(ctx);
         return rc;
     }
+    ctx->stage[0].stream = ctx->stream;
     *out = ctx;
     return MTCP_GPU_OK;
 }
 
 void mtcp_gpu_close(mtcp_gpu_ctx *ctx) {
     if (!ctx) return;
+    DeviceGuard dg(ctx->device);
+    if (!ctx->abandoned) {
+        // the context's own work finishes first (within its wait limit, if
+        // it has one: a device that does not finish it gets the context
+        // abandoned instead).  Work the caller queued on its own streams is
+        // not waited for: the RSS tables it may read are never freed
+        // (rss_tables_for), every other buffer of such a launch is the caller's.
+        const Deadline dl(ctx->wait_us);
+        for (auto &s : ctx->stage)
+            if (s.own_stream && drain(s.stream, dl) == MTCP_GPU_ETIMEDOUT) ctx->abandoned = true;
+        if (ctx->stream && drain(ctx->stream, dl) == MTCP_GPU_ETIMEDOUT) ctx->abandoned = true;
+    }
     if (ctx->abandoned) {
-        // work a timed-out call gave up on may still copy into the staging:
+        // work a timed-out wait gave up on may still copy into the staging:
         // leave every stream and buffer allocated (never touched again)
         // rather than block on a device that stopped answering or free
         // memory under its DMA; only the host-side struct goes
         delete ctx;
         return;
     }
-    DeviceGuard dg(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     // every buffer goes back to park.hpp: a free here would wait for the
     // other contexts' work on the device
     for (auto &s : ctx->stage) {
-        if (s.stream) {
-            (void)hipStreamSynchronize(s.stream);
-            (void)hipStreamDestroy(s.stream);
-        }
+        if (s.own_stream) (void)hipStreamDestroy(s.stream);
         stage_release_buf(s);
         stage_release_pkts(s);
+        stage_release_host(s);
     }
     mtcp_park::release(ctx->h_gather, ctx->h_gather_cap, mtcp_park::kHost);
     mtcp_park::release(ctx->h_gather_desc, (size_t)ctx->h_gather_desc_cap * sizeof(mtcp_gpu_desc),
                        mtcp_park::kHost);
-    mtcp_park::release(ctx->d_rss_tables, mg::kRssTableWords * sizeof(uint32_t), mtcp_park::kDevice);
-    mtcp_park::release(ctx->d_count, sizeof(uint32_t), mtcp_park::kDevice);
-    if (ctx->done_evt) (void)hipEventDestroy(ctx->done_evt);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
+int mtcp_gpu_set_wait_limit(mtcp_gpu_ctx *ctx, uint32_t timeout_us) {
+    if (!ctx) return MTCP_GPU_EINVAL;
+    ctx->wait_us = timeout_us;
+    return MTCP_GPU_OK;
+}
+
+uint32_t mtcp_gpu_wait_limit(const mtcp_gpu_ctx *ctx) { return ctx ? ctx->wait_us : 0u; }
+
 int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
     if (!ctx) return MTCP_GPU_EINVAL;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     DeviceGuard dg(ctx->device);
     if (!dg.ok) return MTCP_GPU_ENODEV;
+    const Deadline dl(ctx->wait_us);
     // a host call's batches span at most kStageBytes / kStagePkts and start
     // at stage 0; later stages are used only by calls larger than one stage
     const uint64_t bytes = std::min(max_bytes, kStageBytes);
@@ -468,25 +656,26 @@ int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
                        : max_bytes > kStageBytes || max_pkts > kStagePkts ? kStages
                                                                           : 1;
     for (int i = 0; i < stages; ++i) {
-        const int rc = stage_reserve(ctx, ctx->stage[i], ((bytes + 15) & ~15ull) + 16, std::max(pkts, 1u));
+        const int rc = stage_reserve(ctx, ctx->stage[i], ((bytes + 15) & ~15ull) + 16, std::max(pkts, 1u), dl);
         if (rc != MTCP_GPU_OK) return rc;
     }
     // a stream sets up its copy queues on its first large copy (7.8 ms
-    // measured): do that here for the stages the host calls use
+    // measured): do that here for the stages the host calls use, with the
+    // pinned buffers a bounded context's calls go through
     const size_t warm = stages ? (size_t)std::min<uint64_t>(ctx->stage[0].buf_cap, 1ull << 20) : 0;
-    void *h = nullptr;
-    if (warm && !HIP_OK(mtcp_park::alloc(&h, warm, mtcp_park::kHost))) return MTCP_GPU_ENOMEM;
-    if (h) memset(h, 0, warm);
-    bool ok = true;
-    for (int i = 0; i < stages && ok && h; ++i) {
+    int rc = MTCP_GPU_OK;
+    for (int i = 0; i < stages && rc == MTCP_GPU_OK; ++i) {
         Stage &st = ctx->stage[i];
-        const size_t w = (size_t)std::min<uint64_t>(warm, st.buf_cap);
-        ok = HIP_OK(hipMemcpyAsync(st.d_buf, h, w, hipMemcpyHostToDevice, st.stream)) &&
-             HIP_OK(hipMemcpyAsync(h, st.d_buf, w, hipMemcpyDeviceToHost, st.stream)) &&
-             HIP_OK(hipStreamSynchronize(st.stream));
+        rc = stage_host(ctx, st, warm, warm, dl);
+        if (rc == MTCP_GPU_OK) {
+            memset(st.h_in, 0, warm);
+            if (!HIP_OK(hipMemcpyAsync(st.d_buf, st.h_in, warm, hipMemcpyHostToDevice, st.stream)) ||
+                !HIP_OK(hipMemcpyAsync(st.h_out, st.d_buf, warm, hipMemcpyDeviceToHost, st.stream)))
+                rc = MTCP_GPU_EIO;
+        }
     }
-    mtcp_park::release(h, warm, mtcp_park::kHost);
-    if (!ok) return MTCP_GPU_EIO;
+    rc = finish_call(ctx, rc, dl, stages);
+    if (rc != MTCP_GPU_OK) return rc;
     // the code object loads on the first launch of any of its kernels
     hipFuncAttributes attr;
     if (!HIP_OK(hipFuncGetAttributes(
@@ -513,16 +702,6 @@ int mtcp_gpu_dev_ioctl(mtcp_gpu_ctx *ctx, int nif, int cmd, void *argp) {
 
 void *mtcp_gpu_stream(mtcp_gpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
-void *mtcp_gpu_host_stream(mtcp_gpu_ctx *ctx) {
-    if (!ctx || ctx->abandoned) return nullptr;
-    Stage &s = ctx->stage[0];
-    if (!s.stream) {
-        DeviceGuard dg(ctx->device);
-        if (!dg.ok || !HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking))) return nullptr;
-    }
-    return (void *)s.stream;
-}
-
 uint32_t mtcp_gpu_record_size(const mtcp_gpu_ctx *ctx) { return ctx ? (uint32_t)record_size(ctx) : 0u; }
 
 const char *mtcp_gpu_last_kernel(const mtcp_gpu_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
@@ -531,7 +710,9 @@ int mtcp_gpu_sync(mtcp_gpu_ctx *ctx) {
     if (!ctx) return MTCP_GPU_EINVAL;
     if (ctx->abandoned) return MTCP_GPU_EIO;
     DeviceGuard dg(ctx->device);
-    return HIP_OK(hipStreamSynchronize(ctx->stream)) ? MTCP_GPU_OK : MTCP_GPU_EIO;
+    // with a wait limit: MTCP_GPU_ETIMEDOUT past it, and the context stays
+    // usable (what is still running is the caller's own device work)
+    return drain(ctx->stream, Deadline(ctx->wait_us));
 }
 
 int mtcp_gpu_rx_chunk_flow_dev(mtcp_gpu_ctx *ctx, const void *d_buf, uint64_t buf_len,
@@ -613,28 +794,50 @@ int mtcp_gpu_tx_fill_dev(mtcp_gpu_ctx *ctx, void *d_buf, uint64_t buf_len,
     return launch<mg::kTxChunk>(ctx, kp, pick(ctx, stream));
 }
 
-// Host-memory rx: batches of packets stream through kStages pinned-device
-// stages, each on its own stream (H2D of batch b+1 overlaps the kernel of b
-// and the D2H of b-1).  Each batch copies only the byte span its packets
-// occupy and the kernel rebases descriptor offsets by that span's start.
-int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
-                      const mtcp_gpu_desc *desc, uint32_t n, uint32_t off_shift,
-                      mtcp_gpu_result *out) {
-    if (!ctx || (n && (!buf || !desc || !out)) || off_shift > 16) return MTCP_GPU_EINVAL;
-    if (n == 0) return MTCP_GPU_OK;
-    DeviceGuard dg(ctx->device);
+}  // extern "C"
+
+namespace {
+
+// Host-memory rx (mtcp_gpu_rx_chunk, _rx_ptrs): batches of packets stream
+// through kStages stages — stage 0 on the context's stream, 1 and 2 on their
+// own — so that the H2D of batch b+1 overlaps the kernel of b and the D2H of
+// b-1.  Each batch copies only the byte span its packets occupy and the
+// kernel rebases descriptor offsets by that span's start.  Unbounded (the
+// context has no wait limit): the copies read the caller's chunk and write
+// its records directly.  Bounded: every byte passes through the stages'
+// pinned bounce buffers (`owned`: buf / desc already are the context's own
+// pinned gather and are not copied again), so that no copy the call gives up
+// on at its deadline can touch the caller's memory afterwards.
+int rx_host(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len, const mtcp_gpu_desc *desc, uint32_t n,
+            uint32_t off_shift, mtcp_gpu_result *out, bool owned, const Deadline &dl) {
     int rc = MTCP_GPU_OK;
     uint8_t *const out_b = reinterpret_cast<uint8_t *>(out);
     const size_t rec = (size_t)record_size(ctx);
+    const bool bounce = dl.bounded;
+    const uint64_t out_bytes = (uint64_t)kStagePkts * rec;
     if (!offsets_sorted(desc, n)) {
         // arbitrary order: stage the whole chunk once, then batches of descriptors
         Stage &s = ctx->stage[0];
-        rc = stage_reserve(ctx, s, ((buf_len + 15) & ~15ull) + 16, kStagePkts);
-        if (rc == MTCP_GPU_OK &&
-            !HIP_OK(hipMemcpyAsync(s.d_buf, buf, buf_len, hipMemcpyHostToDevice, s.stream)))
+        const uint64_t padded = (buf_len + 15) & ~15ull;
+        rc = stage_reserve(ctx, s, padded + 16, kStagePkts, dl);
+        if (rc == MTCP_GPU_OK && bounce)
+            rc = stage_host(ctx, s, owned ? 0 : padded + (uint64_t)kStagePkts * sizeof(mtcp_gpu_desc), out_bytes, dl);
+        const uint8_t *src = buf;
+        if (rc == MTCP_GPU_OK && bounce && !owned) {
+            bounce_in(s.h_in, buf, buf_len);
+            src = s.h_in;
+        }
+        if (rc == MTCP_GPU_OK && !HIP_OK(hipMemcpyAsync(s.d_buf, src, buf_len, hipMemcpyHostToDevice, s.stream)))
             rc = MTCP_GPU_EIO;
         for (uint32_t first = 0; first < n && rc == MTCP_GPU_OK; first += kStagePkts) {
             const uint32_t cnt = std::min(n - first, kStagePkts);
+            if ((rc = stage_collect(ctx, s, out_b, rec, dl)) != MTCP_GPU_OK) break;   // the previous batch
+            const mtcp_gpu_desc *dsrc = desc + first;
+            if (bounce && !owned) {
+                mtcp_gpu_desc *d = reinterpret_cast<mtcp_gpu_desc *>(s.h_in + padded);
+                memcpy(d, desc + first, (size_t)cnt * sizeof(mtcp_gpu_desc));
+                dsrc = d;
+            }
             const mtcp_gpu_size_hint hint = size_hint(desc + first, cnt);
             mg::KParams kp = base_params(ctx);
             kp.buf = s.d_buf;
@@ -643,14 +846,15 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
             kp.n = cnt;
             kp.off_shift = off_shift;
             kp.out = s.d_out;
-            if (!HIP_OK(hipMemcpyAsync(s.d_desc, desc + first, (size_t)cnt * sizeof(mtcp_gpu_desc),
+            if (!HIP_OK(hipMemcpyAsync(s.d_desc, dsrc, (size_t)cnt * sizeof(mtcp_gpu_desc),
                                        hipMemcpyHostToDevice, s.stream)))
                 rc = MTCP_GPU_EIO;
             if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream, &hint);
             if (rc == MTCP_GPU_OK &&
-                !HIP_OK(hipMemcpyAsync(out_b + first * rec, s.d_out, cnt * rec,
+                !HIP_OK(hipMemcpyAsync(bounce ? s.h_out : out_b + first * rec, s.d_out, cnt * rec,
                                        hipMemcpyDeviceToHost, s.stream)))
                 rc = MTCP_GPU_EIO;
+            if (rc == MTCP_GPU_OK && bounce) s.pend_first = first, s.pend_cnt = cnt;
         }
     } else {
         uint32_t first = 0;
@@ -672,9 +876,20 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
             }
             if (!hint.max_len) hint.min_len = 0;
             Stage &s = ctx->stage[b % kStages];
-            const uint64_t span = hi - lo;
-            rc = stage_reserve(ctx, s, ((span + 15) & ~15ull) + 16, kStagePkts);
+            const uint64_t span = hi - lo, padded = (span + 15) & ~15ull;
+            if ((rc = stage_collect(ctx, s, out_b, rec, dl)) != MTCP_GPU_OK) break;   // its batch b - kStages
+            rc = stage_reserve(ctx, s, padded + 16, kStagePkts, dl);
+            if (rc == MTCP_GPU_OK && bounce)
+                rc = stage_host(ctx, s, owned ? 0 : padded + (uint64_t)cnt * sizeof(mtcp_gpu_desc), out_bytes, dl);
             if (rc != MTCP_GPU_OK) break;
+            const uint8_t *src = buf + lo;
+            const mtcp_gpu_desc *dsrc = desc + first;
+            if (bounce && !owned) {
+                bounce_in(s.h_in, buf + lo, span);
+                memcpy(s.h_in + padded, desc + first, (size_t)cnt * sizeof(mtcp_gpu_desc));
+                src = s.h_in;
+                dsrc = reinterpret_cast<const mtcp_gpu_desc *>(s.h_in + padded);
+            }
             mg::KParams kp = base_params(ctx);
             kp.buf = s.d_buf;
             kp.buf_len = span;           // descriptors are bounded by the caller's buf_len
@@ -683,28 +898,25 @@ int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
             kp.n = cnt;
             kp.off_shift = off_shift;
             kp.out = s.d_out;
-            if ((span && !HIP_OK(hipMemcpyAsync(s.d_buf, buf + lo, span, hipMemcpyHostToDevice,
-                                                s.stream))) ||
-                !HIP_OK(hipMemcpyAsync(s.d_desc, desc + first, (size_t)cnt * sizeof(mtcp_gpu_desc),
+            if ((span && !HIP_OK(hipMemcpyAsync(s.d_buf, src, span, hipMemcpyHostToDevice, s.stream))) ||
+                !HIP_OK(hipMemcpyAsync(s.d_desc, dsrc, (size_t)cnt * sizeof(mtcp_gpu_desc),
                                        hipMemcpyHostToDevice, s.stream)))
                 rc = MTCP_GPU_EIO;
             if (rc == MTCP_GPU_OK) rc = launch<mg::kRxChunk>(ctx, kp, s.stream, &hint);
             if (rc == MTCP_GPU_OK &&
-                !HIP_OK(hipMemcpyAsync(out_b + first * rec, s.d_out, cnt * rec,
+                !HIP_OK(hipMemcpyAsync(bounce ? s.h_out : out_b + first * rec, s.d_out, cnt * rec,
                                        hipMemcpyDeviceToHost, s.stream)))
                 rc = MTCP_GPU_EIO;
+            if (rc == MTCP_GPU_OK && bounce) s.pend_first = first, s.pend_cnt = cnt;
             first += cnt;
         }
     }
-    for (auto &s : ctx->stage)
-        if (s.stream && !HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK)
-            rc = MTCP_GPU_EIO;
-    return rc;
+    // a stage_collect that timed out has abandoned the context already: no
+    // more waits (finish_call would wait out nothing new, but the call has
+    // reached its deadline)
+    if (rc == MTCP_GPU_ETIMEDOUT) return rc;
+    return finish_call(ctx, rc, dl, kStages, out_b, rec);
 }
-
-}  // extern "C"
-
-namespace {
 
 // Gather a pointer burst into the context's pinned PSIO-style chunk (64 B
 // aligned slots, pslib.c:146) with its descriptors; *total = chunk bytes.
@@ -744,27 +956,48 @@ int gather_burst(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *
     return MTCP_GPU_OK;
 }
 
+// The two check fields of a filled frame (the tx kernels' report: {ip check
+// | tcp check << 16, T}, T the TCP header's offset, 0 = not filled), written
+// by the calling thread: iph->check (ip_out.c:164), tcph->check (tcp_out.c:329)
+inline void write_checks(uint8_t *frame, uint2 r) {
+    const uint16_t ipc = (uint16_t)r.x, tcpc = (uint16_t)(r.x >> 16);
+    memcpy(frame + 24, &ipc, 2);
+    memcpy(frame + r.y + 16, &tcpc, 2);
+}
+
 }  // namespace
 
 extern "C" {
 
+int mtcp_gpu_rx_chunk(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len,
+                      const mtcp_gpu_desc *desc, uint32_t n, uint32_t off_shift,
+                      mtcp_gpu_result *out) {
+    if (!ctx || (n && (!buf || !desc || !out)) || off_shift > 16) return MTCP_GPU_EINVAL;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
+    if (n == 0) return MTCP_GPU_OK;
+    DeviceGuard dg(ctx->device);
+    return rx_host(ctx, buf, buf_len, desc, n, off_shift, out, false, Deadline(ctx->wait_us));
+}
+
 int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *lens,
                      uint32_t n, mtcp_gpu_result *out) {
     if (!ctx || (n && (!pkts || !lens || !out))) return MTCP_GPU_EINVAL;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
+    const Deadline dl(ctx->wait_us);
     uint64_t total = 0;
     const int rc = gather_burst(ctx, pkts, lens, n, &total);
     if (rc != MTCP_GPU_OK) return rc;
-    return mtcp_gpu_rx_chunk(ctx, ctx->h_gather, total, ctx->h_gather_desc, n, 6, out);
+    return rx_host(ctx, ctx->h_gather, total, ctx->h_gather_desc, n, 6, out, true, dl);
 }
 
 // tx fill of a host pointer burst (a DPDK wmbufs[].m_table, dpdk_module.c:341-370):
 // the frames are gathered into pinned staging and checked on the GPU, which
-// reports {checks, T} per frame (rx_wave_kernel report mode); only the two
+// reports {checks, T} per frame (the tx kernels' report mode); only the two
 // check fields are written back into the caller's frames, here on the host,
-// once the report is in.  With a limit (timeout_us > 0) the wait for the
-// report polls a completion event: past the limit nothing has been written
+// once the report is in.  With a limit (timeout_us, else the context's wait
+// limit) the wait polls the device: past the limit nothing has been written
 // into the caller's frames, the call answers MTCP_GPU_ETIMEDOUT and the
 // context is abandoned (the copies may still run into its staging).  mTCP's
 // own tx fill never waits on a device (tcp_out.c:320-329, ip_out.c:147-165,
@@ -776,15 +1009,13 @@ int mtcp_gpu_tx_fill_ptrs_for(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uin
     if (ctx->abandoned) return MTCP_GPU_EIO;
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
+    const Deadline dl(timeout_us ? timeout_us : ctx->wait_us);
     uint64_t total = 0;
     int rc = gather_burst(ctx, pkts, lens, n, &total);
     if (rc != MTCP_GPU_OK) return rc;
     Stage &s = ctx->stage[0];
-    rc = stage_reserve(ctx, s, ((total + 15) & ~15ull) + 16, n);
+    rc = stage_reserve(ctx, s, ((total + 15) & ~15ull) + 16, n, dl);
     if (rc != MTCP_GPU_OK) return rc;
-    if (timeout_us && !ctx->done_evt &&
-        !HIP_OK(hipEventCreateWithFlags(&ctx->done_evt, hipEventDisableTiming)))
-        return MTCP_GPU_EIO;
     uint2 *report = reinterpret_cast<uint2 *>(ctx->h_gather_desc);    // reused once the H2D is done
     static_assert(sizeof(uint2) == sizeof(mtcp_gpu_desc), "report reuses the descriptor staging");
     if (!HIP_OK(hipMemcpyAsync(s.d_buf, ctx->h_gather, total, hipMemcpyHostToDevice, s.stream)) ||
@@ -802,31 +1033,14 @@ int mtcp_gpu_tx_fill_ptrs_for(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uin
     if (rc == MTCP_GPU_OK && !HIP_OK(hipMemcpyAsync(report, s.d_out, (size_t)n * sizeof(uint2),
                                                     hipMemcpyDeviceToHost, s.stream)))
         rc = MTCP_GPU_EIO;
-    if (timeout_us && rc == MTCP_GPU_OK) {
-        if (!HIP_OK(hipEventRecord(ctx->done_evt, s.stream))) rc = MTCP_GPU_EIO;
-        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
-        while (rc == MTCP_GPU_OK) {
-            const hipError_t e = hipEventQuery(ctx->done_evt);
-            if (e == hipSuccess) break;
-            if (e != hipErrorNotReady) {
-                rc = MTCP_GPU_EIO;
-            } else if (std::chrono::steady_clock::now() >= deadline) {
-                ctx->abandoned = true;
-                return MTCP_GPU_ETIMEDOUT;
-            }
-        }
-    }
-    // an enqueue that failed still drains the stream: a queued H2D may be
-    // reading the staging (unbounded, as in every call without a limit)
-    if (!HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK) rc = MTCP_GPU_EIO;
+    // every path drains the stream within the deadline, a failed enqueue's
+    // too: an H2D already queued may be reading the staging
+    rc = finish_call(ctx, rc, dl, 1);
     if (rc != MTCP_GPU_OK) return rc;
     uint32_t cnt = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t T = report[i].y;
-        if (!T) continue;
-        const uint16_t ipc = (uint16_t)report[i].x, tcpc = (uint16_t)(report[i].x >> 16);
-        memcpy(pkts[i] + 24, &ipc, 2);                                 // iph->check   (ip_out.c:164)
-        memcpy(pkts[i] + T + 16, &tcpc, 2);                            // tcph->check  (tcp_out.c:329)
+        if (!report[i].y) continue;
+        write_checks(pkts[i], report[i]);
         ++cnt;
     }
     if (n_filled) *n_filled = cnt;
@@ -838,23 +1052,41 @@ int mtcp_gpu_tx_fill_ptrs(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uint16_
     return mtcp_gpu_tx_fill_ptrs_for(ctx, pkts, lens, n, n_filled, 0);
 }
 
+// tx fill of a host chunk, in place: the chunk goes to the GPU once, the
+// kernel reports {checks, T} per frame (n x 8 B back instead of the whole
+// chunk) and the calling thread writes the two check fields of each filled
+// frame.  Bounded (a context wait limit): the chunk and the descriptors are
+// copied into pinned bounce buffers first, so that no copy given up on at
+// the deadline reads the caller's memory later, and nothing is written into
+// the chunk unless the report came in time.
 int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mtcp_gpu_desc *desc,
                      uint32_t n, uint32_t off_shift, uint32_t *n_filled) {
     if (!ctx || (n && (!buf || !desc)) || off_shift > 16) return MTCP_GPU_EINVAL;
     if (n_filled) *n_filled = 0;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
+    const Deadline dl(ctx->wait_us);
+    const bool bounce = dl.bounded;
     Stage &s = ctx->stage[0];
-    const uint64_t cap = (buf_len + 15) & ~15ull;
-    int rc = stage_reserve(ctx, s, cap + 16, n);
+    const uint64_t padded = (buf_len + 15) & ~15ull;
+    const uint64_t dbytes = (uint64_t)n * sizeof(mtcp_gpu_desc);
+    int rc = stage_reserve(ctx, s, padded + 16, n, dl);
+    if (rc == MTCP_GPU_OK) rc = stage_host(ctx, s, bounce ? padded + dbytes : 0, (uint64_t)n * sizeof(uint2), dl);
     if (rc != MTCP_GPU_OK) return rc;
-    // an enqueue that fails still drains the stream below: an H2D already
-    // queued may be reading the caller's buf
+    const uint8_t *src = buf;
+    const mtcp_gpu_desc *dsrc = desc;
+    if (bounce) {
+        bounce_in(s.h_in, buf, buf_len);
+        memcpy(s.h_in + padded, desc, dbytes);
+        src = s.h_in;
+        dsrc = reinterpret_cast<const mtcp_gpu_desc *>(s.h_in + padded);
+    }
+    // the 16 B past the chunk (the kernels' last vector load of a frame
+    // ending there) read as zeros
     if (!HIP_OK(hipMemsetAsync(s.d_buf + (buf_len & ~15ull), 0, 16, s.stream)) ||
-        !HIP_OK(hipMemcpyAsync(s.d_buf, buf, buf_len, hipMemcpyHostToDevice, s.stream)) ||
-        !HIP_OK(hipMemcpyAsync(s.d_desc, desc, (size_t)n * sizeof(mtcp_gpu_desc),
-                               hipMemcpyHostToDevice, s.stream)) ||
-        !HIP_OK(hipMemsetAsync(ctx->d_count, 0, sizeof(uint32_t), s.stream)))
+        !HIP_OK(hipMemcpyAsync(s.d_buf, src, buf_len, hipMemcpyHostToDevice, s.stream)) ||
+        !HIP_OK(hipMemcpyAsync(s.d_desc, dsrc, dbytes, hipMemcpyHostToDevice, s.stream)))
         rc = MTCP_GPU_EIO;
     mg::KParams kp = base_params(ctx);
     kp.buf = s.d_buf;
@@ -862,16 +1094,24 @@ int mtcp_gpu_tx_fill(mtcp_gpu_ctx *ctx, uint8_t *buf, uint64_t buf_len, const mt
     kp.desc = s.d_desc;
     kp.n = n;
     kp.off_shift = off_shift;
-    kp.fill_count = ctx->d_count;
+    kp.tx_report = reinterpret_cast<uint2 *>(s.d_out);                // n x 8 B <= n x 40 B
+    uint2 *report = reinterpret_cast<uint2 *>(s.h_out);
     if (rc == MTCP_GPU_OK) rc = launch<mg::kTxChunk>(ctx, kp, s.stream);
-    uint32_t cnt = 0;
-    if (rc == MTCP_GPU_OK &&
-        (!HIP_OK(hipMemcpyAsync(buf, s.d_buf, buf_len, hipMemcpyDeviceToHost, s.stream)) ||
-         !HIP_OK(hipMemcpyAsync(&cnt, ctx->d_count, sizeof(cnt), hipMemcpyDeviceToHost, s.stream))))
+    if (rc == MTCP_GPU_OK && !HIP_OK(hipMemcpyAsync(report, s.d_out, (size_t)n * sizeof(uint2),
+                                                    hipMemcpyDeviceToHost, s.stream)))
         rc = MTCP_GPU_EIO;
-    if (!HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK) rc = MTCP_GPU_EIO;
-    if (rc == MTCP_GPU_OK && n_filled) *n_filled = cnt;
-    return rc;
+    rc = finish_call(ctx, rc, dl, 1);
+    if (rc != MTCP_GPU_OK) return rc;
+    uint32_t cnt = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t off = (uint64_t)desc[i].offset << off_shift;
+        // the kernel reports only frames inside the chunk (checked again here)
+        if (!report[i].y || off + report[i].y + 18 > buf_len) continue;
+        write_checks(buf + off, report[i]);
+        ++cnt;
+    }
+    if (n_filled) *n_filled = cnt;
+    return MTCP_GPU_OK;
 }
 
 // ---- flow-table hash --------------------------------------
@@ -893,20 +1133,30 @@ int mtcp_gpu_flow_hash_dev(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *d_res, uint
 int mtcp_gpu_flow_hash(mtcp_gpu_ctx *ctx, const mtcp_gpu_result *res, uint32_t n,
                        uint32_t *bins) {
     if (!ctx || (n && (!res || !bins)) || (ctx->flags & MTCP_GPU_F_COMPACT)) return MTCP_GPU_EINVAL;
+    if (ctx->abandoned) return MTCP_GPU_EIO;
     if (n == 0) return MTCP_GPU_OK;
     DeviceGuard dg(ctx->device);
+    const Deadline dl(ctx->wait_us);
+    const bool bounce = dl.bounded;
+    const uint64_t rbytes = (uint64_t)n * sizeof(mtcp_gpu_result), bbytes = (uint64_t)n * sizeof(uint32_t);
     Stage &s = ctx->stage[0];
-    int rc = stage_reserve(ctx, s, (uint64_t)n * sizeof(uint32_t), n);
+    int rc = stage_reserve(ctx, s, bbytes, n, dl);
+    if (rc == MTCP_GPU_OK && bounce) rc = stage_host(ctx, s, rbytes, bbytes, dl);
     if (rc != MTCP_GPU_OK) return rc;
+    const void *src = res;
+    if (bounce) {
+        memcpy(s.h_in, res, rbytes);
+        src = s.h_in;
+    }
     uint32_t *d_bins = reinterpret_cast<uint32_t *>(s.d_buf);
-    if (!HIP_OK(hipMemcpyAsync(s.d_out, res, (size_t)n * sizeof(mtcp_gpu_result),
-                               hipMemcpyHostToDevice, s.stream)))
+    if (!HIP_OK(hipMemcpyAsync(s.d_out, src, rbytes, hipMemcpyHostToDevice, s.stream)))
         rc = MTCP_GPU_EIO;
     if (rc == MTCP_GPU_OK) rc = mtcp_gpu_flow_hash_dev(ctx, s.d_out, n, d_bins, s.stream);
-    if (rc == MTCP_GPU_OK && !HIP_OK(hipMemcpyAsync(bins, d_bins, (size_t)n * sizeof(uint32_t),
+    if (rc == MTCP_GPU_OK && !HIP_OK(hipMemcpyAsync(bounce ? (void *)s.h_out : (void *)bins, d_bins, bbytes,
                                                     hipMemcpyDeviceToHost, s.stream)))
         rc = MTCP_GPU_EIO;
-    if (!HIP_OK(hipStreamSynchronize(s.stream)) && rc == MTCP_GPU_OK) rc = MTCP_GPU_EIO;
+    rc = finish_call(ctx, rc, dl, 1);
+    if (rc == MTCP_GPU_OK && bounce) memcpy(bins, s.h_out, bbytes);
     return rc;
 }
 
@@ -960,12 +1210,16 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues, uint3
     uint32_t *d_counts = reinterpret_cast<uint32_t *>(d_mem + qbytes);
     mtcp_gpu_addr_entry *d_out = reinterpret_cast<mtcp_gpu_addr_entry *>(d_mem + out_off);
     hipStream_t st = ctx->stream;
+    const Deadline dl(ctx->wait_us);
+    Stage &s0 = ctx->stage[0];                                             // its stream is st
     const uint32_t saddr_base_h = __builtin_bswap32(saddr_base);           // addr_pool.c:150
     int rc = mtcp_gpu_rss_queue_map_dev(ctx, saddr_base_h, (uint32_t)num_addr,
                                         __builtin_bswap32(daddr),
                                         (uint16_t)((dport >> 8) | (dport << 8)), num_queues,
                                         endian_check, d_queue, st);
-    uint32_t count = 0;
+    // what comes back lands in the stage's pinned buffer first (the count,
+    // then the entries), copied out once its copy has finished
+    if (rc == MTCP_GPU_OK) rc = stage_host(ctx, s0, 0, 8ull * std::max(limit, 1u), dl);
     if (rc == MTCP_GPU_OK) {
         hipLaunchKernelGGL(mg::pool_count_kernel, dim3(nb), dim3(mg::kBlock), 0, st, d_queue, total,
                            (uint32_t)core, d_counts);
@@ -974,19 +1228,27 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues, uint3
             hipLaunchKernelGGL(mg::pool_emit_kernel, dim3(nb), dim3(mg::kBlock), 0, st, d_queue,
                                total, (uint32_t)core, d_counts, saddr_base_h, limit, d_out);
         if (!HIP_OK(hipGetLastError()) ||
-            !HIP_OK(hipMemcpyAsync(&count, d_counts + nb, sizeof(count), hipMemcpyDeviceToHost, st)))
+            !HIP_OK(hipMemcpyAsync(s0.h_out, d_counts + nb, sizeof(uint32_t), hipMemcpyDeviceToHost, st)))
             rc = MTCP_GPU_EIO;
-        if (rc == MTCP_GPU_OK && !HIP_OK(hipStreamSynchronize(st))) rc = MTCP_GPU_EIO;
+        rc = finish_call(ctx, rc, dl, 1);
+    }
+    if (rc == MTCP_GPU_OK) {
+        uint32_t count;
+        memcpy(&count, s0.h_out, sizeof(count));
         const uint32_t kept = std::min(count, num_entry);
         const uint32_t copy = std::min(kept, max_out);
-        if (rc == MTCP_GPU_OK && copy &&
-            !HIP_OK(hipMemcpy(out, d_out, (size_t)copy * sizeof(mtcp_gpu_addr_entry),
-                              hipMemcpyDeviceToHost)))
+        if (copy && !HIP_OK(hipMemcpyAsync(s0.h_out, d_out, (size_t)copy * sizeof(mtcp_gpu_addr_entry),
+                                           hipMemcpyDeviceToHost, st)))
             rc = MTCP_GPU_EIO;
-        if (rc == MTCP_GPU_OK) *n_found = kept;
+        rc = finish_call(ctx, rc, dl, 1);
+        if (rc == MTCP_GPU_OK) {
+            memcpy(out, s0.h_out, (size_t)copy * sizeof(mtcp_gpu_addr_entry));
+            *n_found = kept;
+        }
     }
-    (void)hipStreamSynchronize(st);
-    mtcp_park::release(d_mem, bytes, mtcp_park::kDevice);
+    if (rc == MTCP_GPU_ETIMEDOUT) return rc;                 // abandoned: d_mem stays allocated
+    if (rc != MTCP_GPU_OK) (void)finish_call(ctx, rc, dl, 1);
+    if (!ctx->abandoned) mtcp_park::release(d_mem, bytes, mtcp_park::kDevice);
     return rc;
 }
 

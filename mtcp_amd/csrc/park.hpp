@@ -16,9 +16,12 @@
 //
 // Bounds: buffers above kParkMaxBytes (a bench-sized reserve) are freed as
 // before, and at most kParkDeviceBytes of each kind (pinned host, device)
-// are parked per device (past that a release frees).  The caller has made
-// the buffer's device current and has finished its own work on the buffer
-// (its streams are synchronised).
+// are parked per device (past that a release frees).  A parked buffer is
+// handed to the smallest request it covers up to twice over (best fit), so
+// that a process whose sizes vary (a sweep of rxq sizes, the tests) reuses
+// what it parked instead of filling the park with sizes that never match
+// again.  The caller has made the buffer's device current and has finished
+// its own work on the buffer (its streams are synchronised).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -43,7 +46,8 @@ struct Parked {
 
 struct Pool {
     std::mutex m;
-    std::vector<Parked> bufs;
+    std::vector<Parked> bufs;        // parked
+    std::vector<Parked> lent;        // handed out larger than asked: their real size
     size_t parked[kParkDevices][2] = {};
 };
 
@@ -58,23 +62,29 @@ inline int current_device() {
     return hipGetDevice(&d) == hipSuccess ? d : -1;
 }
 
-// hipMalloc / hipHostMalloc(hipHostMallocDefault) of `bytes`, or a parked
-// buffer of exactly that size on the current device
+// hipMalloc / hipHostMalloc(hipHostMallocDefault) of `bytes`, or the
+// smallest parked buffer of `bytes` to 2 x `bytes` on the current device
 inline hipError_t alloc(void **out, size_t bytes, Kind kind) {
     *out = nullptr;
     const int dev = current_device();
     if (dev >= 0 && dev < kParkDevices && bytes <= kParkMaxBytes) {
         Pool &pl = pool();
         std::lock_guard<std::mutex> lk(pl.m);
-        for (size_t i = pl.bufs.size(); i-- > 0;) {
+        size_t best = pl.bufs.size();
+        for (size_t i = 0; i < pl.bufs.size(); ++i) {
             const Parked &b = pl.bufs[i];
-            if (b.device == dev && b.kind == kind && b.bytes == bytes) {
-                *out = b.p;
-                pl.parked[dev][kind] -= bytes;
-                pl.bufs[i] = pl.bufs.back();
-                pl.bufs.pop_back();
-                return hipSuccess;
-            }
+            if (b.device == dev && b.kind == kind && b.bytes >= bytes && b.bytes / 2 <= bytes &&
+                (best == pl.bufs.size() || b.bytes < pl.bufs[best].bytes))
+                best = i;
+        }
+        if (best < pl.bufs.size()) {
+            const Parked b = pl.bufs[best];
+            *out = b.p;
+            pl.parked[dev][kind] -= b.bytes;
+            pl.bufs[best] = pl.bufs.back();
+            pl.bufs.pop_back();
+            if (b.bytes != bytes) pl.lent.push_back(b);
+            return hipSuccess;
         }
     }
     return kind == kHost ? hipHostMalloc(out, bytes, hipHostMallocDefault) : hipMalloc(out, bytes);
@@ -88,14 +98,22 @@ inline hipError_t alloc(T **out, size_t bytes, Kind kind) {
     return e;
 }
 
-// give back a buffer alloc() returned (with the same size and kind)
+// give back a buffer alloc() returned (with the size it was asked for)
 inline void release(void *p, size_t bytes, Kind kind) {
     if (!p) return;
     const int dev = current_device();
-    if (dev >= 0 && dev < kParkDevices && bytes <= kParkMaxBytes) {
-        Pool &pl = pool();
+    Pool &pl = pool();
+    {
         std::lock_guard<std::mutex> lk(pl.m);
-        if (pl.parked[dev][kind] + bytes <= kParkDeviceBytes) {
+        for (size_t i = 0; i < pl.lent.size(); ++i)
+            if (pl.lent[i].p == p) {
+                bytes = pl.lent[i].bytes;            // the buffer's real size
+                pl.lent[i] = pl.lent.back();
+                pl.lent.pop_back();
+                break;
+            }
+        if (dev >= 0 && dev < kParkDevices && bytes <= kParkMaxBytes &&
+            pl.parked[dev][kind] + bytes <= kParkDeviceBytes) {
             pl.bufs.push_back({dev, kind, bytes, p});
             pl.parked[dev][kind] += bytes;
             return;

@@ -25,6 +25,9 @@
 #include "../../include/mtcp_gpu_rxq.h"
 #include "host_copy.hpp"
 #include "park.hpp"
+#include "wait.hpp"
+
+using mtcp_wait::Deadline;
 
 // get_rptr serves frame i; the header of frame i + kServeAhead is fetched
 // meanwhile (the staged frames were written with streaming stores, so each
@@ -49,6 +52,7 @@ struct mtcp_gpu_rxq {
     uint32_t done_n = 0;                 // frames with results
     uint32_t inflight = 0;               // frames of an unfinished flush_async (0: none)
     bool abandoned = false;              // a flush timed out in rxq_wait_for: no more flushes
+    uint32_t wait_us = 0;                // the context's wait limit at create (0: none)
     uint64_t used = 0;                   // staging bytes in use
     // the frames staged since the last flush: smallest and largest non-zero
     // length, the size hint of their launch (mtcp_gpu_size_hint)
@@ -110,6 +114,7 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     q->max_bytes = (max_bytes + 63) & ~63ull;
     q->stream = reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx));
     q->rec = mtcp_gpu_record_size(ctx);
+    q->wait_us = mtcp_gpu_wait_limit(ctx);
     if (const char *e = getenv("MTCP_GPU_STAGE")) q->plain = strcmp(e, "plain") == 0;
     if (const char *e = getenv("MTCP_GPU_SERVE_AHEAD")) q->ahead = (uint32_t)atoi(e);
     if (const char *e = getenv("MTCP_GPU_SERVE_HINT")) q->hint = (uint32_t)atoi(e);
@@ -137,9 +142,17 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     memset(q->buf, 0, h2d);
     if (rc == MTCP_GPU_OK &&
         (hipMemcpyAsync(q->d_buf, q->buf, h2d, hipMemcpyHostToDevice, q->stream) != hipSuccess ||
-         hipMemcpyAsync(q->res, q->d_out, d2h, hipMemcpyDeviceToHost, q->stream) != hipSuccess ||
-         hipStreamSynchronize(q->stream) != hipSuccess))
+         hipMemcpyAsync(q->res, q->d_out, d2h, hipMemcpyDeviceToHost, q->stream) != hipSuccess))
         rc = MTCP_GPU_EIO;
+    {
+        // (a failed enqueue drains too: a copy already queued uses the staging)
+        const int w = mtcp_wait::drain(q->stream, Deadline(q->wait_us));
+        if (w == MTCP_GPU_ETIMEDOUT) {
+            delete q;                            // the copies may still run: the buffers stay
+            return w;
+        }
+        if (rc == MTCP_GPU_OK) rc = w;
+    }
     if (rc != MTCP_GPU_OK) {
         mtcp_gpu_rxq_destroy(q);
         return rc;
@@ -169,7 +182,12 @@ void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q) {
         }
     }
     if (q->evt) {
-        if (q->inflight) (void)hipEventSynchronize(q->evt);
+        // a flush still in flight finishes first (within the context's wait
+        // limit; past it the buffers stay, as after a timeout above)
+        if (q->inflight && mtcp_wait::wait_event(q->evt, Deadline(q->wait_us)) == MTCP_GPU_ETIMEDOUT) {
+            delete q;
+            return;
+        }
         (void)hipEventDestroy(q->evt);
     }
     // parked, not freed (park.hpp): hipFree / hipHostFree would wait for
@@ -246,7 +264,8 @@ int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
          hipEventRecord(q->evt, q->stream) != hipSuccess))
         rc = MTCP_GPU_EIO;
     if (rc != MTCP_GPU_OK) {
-        (void)hipStreamSynchronize(q->stream);
+        // the copies already queued finish before the staging is touched again
+        if (mtcp_wait::drain(q->stream, Deadline(q->wait_us)) == MTCP_GPU_ETIMEDOUT) q->abandoned = true;
         return rc;
     }
     q->inflight = cnt;
@@ -257,42 +276,21 @@ int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
 
 int mtcp_gpu_rxq_wait(mtcp_gpu_rxq *q, uint32_t *n) {
     if (!q) return MTCP_GPU_EINVAL;
-    int rc = MTCP_GPU_OK;
-    if (q->inflight) {
-        RxqDevice dg(q->device);
-        if (hipEventSynchronize(q->evt) == hipSuccess)
-            q->done_n += q->inflight;
-        else
-            rc = MTCP_GPU_EIO;
-        q->inflight = 0;
-    }
-    if (n) *n = q->done_n;
-    return rc;
+    return mtcp_gpu_rxq_wait_for(q, n, 0);
 }
 
 int mtcp_gpu_rxq_wait_for(mtcp_gpu_rxq *q, uint32_t *n, uint32_t timeout_us) {
     if (!q) return MTCP_GPU_EINVAL;
-    if (!q->inflight || timeout_us == 0) return mtcp_gpu_rxq_wait(q, n);
-    RxqDevice dg(q->device);
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
     int rc = MTCP_GPU_OK;
-    for (;;) {
-        const hipError_t e = hipEventQuery(q->evt);
-        if (e == hipSuccess) {
+    if (q->inflight) {
+        RxqDevice dg(q->device);
+        rc = mtcp_wait::wait_event(q->evt, Deadline(timeout_us ? timeout_us : q->wait_us));
+        if (rc == MTCP_GPU_OK)
             q->done_n += q->inflight;
-            break;
-        }
-        if (e != hipErrorNotReady) {
-            rc = MTCP_GPU_EIO;
-            break;
-        }
-        if (std::chrono::steady_clock::now() >= deadline) {
+        else if (rc == MTCP_GPU_ETIMEDOUT)
             q->abandoned = true;              // its results may still arrive: never read them
-            rc = MTCP_GPU_ETIMEDOUT;
-            break;
-        }
+        q->inflight = 0;
     }
-    q->inflight = 0;
     if (n) *n = q->done_n;
     return rc;
 }

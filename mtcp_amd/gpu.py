@@ -86,6 +86,16 @@ class Context:
             lib().mtcp_gpu_close(self._h)
             self._h = ctypes.c_void_p()
 
+    @property
+    def wait_limit(self) -> int:
+        """The bound of every wait of this context's synchronous calls, in us
+        (0: none; mtcp_gpu_set_wait_limit)."""
+        return lib().mtcp_gpu_wait_limit(self._h)
+
+    @wait_limit.setter
+    def wait_limit(self, timeout_us: int) -> None:
+        check(lib().mtcp_gpu_set_wait_limit(self._h, timeout_us), "mtcp_gpu_set_wait_limit")
+
     def reserve(self, max_bytes: int, max_pkts: int) -> None:
         """Allocate the host calls' device staging and load the kernels now
         (mtcp_gpu_reserve), instead of on the first host-buffer call."""
@@ -210,7 +220,7 @@ class Context:
         `offsets` (a DPDK-style pointer burst into one host buffer); fills
         `buf` in place and returns the number of frames filled.  With
         timeout_us: mtcp_gpu_tx_fill_ptrs_for (MtcpGpuError ETIMEDOUT past
-        the limit, the context abandoned)."""
+        the limit, the context abandoned; 0: the context's wait limit)."""
         offsets = np.asarray(offsets, dtype=np.int64)
         n = len(offsets)
         ptrs = (ctypes.c_void_p * max(n, 1))(*[buf.ctypes.data + int(o) for o in offsets])

@@ -38,10 +38,12 @@
  * dev_ioctl(PKT_RX_IP_CSUM / PKT_RX_TCP_CSUM) answers 0 while the GPU path
  * of that interface is healthy and -1 otherwise, so mTCP falls back to its
  * own checksums exactly as with a NIC that lacks the offload
- * (dpdk_dev_ioctl, dpdk_module.c:809-816).  Every wait on the GPU, receive
- * and transmit, is bounded (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000, 0: none;
- * clamped to 4294967): a GPU that stops answering is abandoned, never waited
- * on again, and mTCP checks and fills every frame from then on.
+ * (dpdk_dev_ioctl, dpdk_module.c:809-816).  Every wait on the GPU — receive,
+ * transmit, init_handle's and destroy_handle's — is bounded
+ * (MTCP_GPU_WAIT_TIMEOUT_MS, default 2000, 0: none; clamped to 4294967; set
+ * on the thread's context with mtcp_gpu_set_wait_limit): a GPU that stops
+ * answering is abandoned, never waited on again, and mTCP checks and fills
+ * every frame from then on.
  * NETSTAT: a frame dropped here never reaches ProcessPacket, so get_rptr
  * counts it in rx_packets / rx_bytes as ProcessPacket would have
  * (eth_in.c:20-23) and core.c:774-775 counts the NULL in rx_errors: the three
@@ -82,7 +84,12 @@
  * with tests/c/libmtcp_gpu_testing.so); a production build ignores those
  * variables.
  *
- * Resources per mTCP thread: one GPU context (one HIP stream), and, for each
+ * Resources per mTCP thread: one GPU context with one HIP stream, which
+ * carries the thread's rx aggregates and its tx fills alike (with the
+ * default two offloading threads a GPU's streams take two of the
+ * GPU_MAX_HW_QUEUES hardware queues, 4 by default, so one thread's stalled
+ * GPU work never delays the other's; an admission past the queue count is
+ * logged with TRACE_CONFIG), and, for each
  * of the CONFIG.eths_num interfaces (mtcp.h:138), two rxqs (pinned staging
  * of GPU_AGG_BURSTS x GPU_BURST frames of up to GPU_FRAME_MAX bytes each,
  * plus a device copy), created at init_handle, off the data path (a pinned
@@ -112,6 +119,8 @@
 #define GPU_FRAME_JUMBO 9216ull           /* the largest frame a burst is expected to bring */
 #define GPU_TX_MAX     4096               /* frames recorded between two send_pkts */
 #define GPU_THREADS_DEFAULT 2             /* offloading threads per GPU */
+#define GPU_STREAMS_PER_THREAD 1          /* a thread's GPU context runs its rx aggregates and
+                                             tx fills on its one stream (include/mtcp_gpu.h) */
 
 /* the backend being wrapped (e.g. &ps_module_func or &dpdk_module_func) */
 io_module_func *gpu_inner_module;
@@ -308,15 +317,37 @@ static int gpu_thread_limit(void)
     return atoi(lim) < 0 ? 0 : atoi(lim);
 }
 
+/* Returns the thread's place among the device's offloading threads (1, 2,
+ * ...), or 0 when it is refused. */
 static int gpu_thread_admit(int dev)
 {
     const int lim = gpu_thread_limit();         /* -1: no limit (still counted) */
+    int n;
     if (dev < 0 || dev >= GPU_TOPO_MAX_DEVS)
         return 1;
-    if (__sync_add_and_fetch(&gpu_thread_count[dev], 1) <= lim || lim < 0)
-        return 1;
+    n = __sync_add_and_fetch(&gpu_thread_count[dev], 1);
+    if (n <= lim || lim < 0)
+        return n;
     __sync_sub_and_fetch(&gpu_thread_count[dev], 1);
     return 0;
+}
+
+/* HIP maps a process's streams on a device onto GPU_MAX_HW_QUEUES hardware
+ * queues (4 unless the environment sets it).  Up to that many streams never
+ * share one, so a thread whose GPU work stalls holds up no other thread's;
+ * past it two threads' streams can share a queue and one's stall delays the
+ * other's aggregates.  True when the n-th offloading thread on a device is
+ * past that point. */
+static int gpu_hw_queues(void)
+{
+    const char *e = getenv("GPU_MAX_HW_QUEUES");
+    int q = e && *e ? atoi(e) : 4;
+    return q > 0 ? q : 4;
+}
+
+static int gpu_queues_shared(int n)
+{
+    return n * GPU_STREAMS_PER_THREAD > gpu_hw_queues();
 }
 
 static void gpu_thread_release(struct gpu_private_context *g)
@@ -344,7 +375,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
     struct gpu_private_context *g = calloc(1, sizeof(*g));
     const char *pl = getenv("MTCP_GPU_PIPELINE");
     const char *tx = getenv("MTCP_GPU_TX");
-    int ndev, dev, i;
+    int ndev, dev, place, i;
 
     gpu_inner_module->init_handle(ctx);       /* sets ctx->io_private_context */
     if (!g) {
@@ -372,7 +403,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
     g->stall_after = getenv("MTCP_GPU_STALL_AFTER") ? atol(getenv("MTCP_GPU_STALL_AFTER")) : -1;
     g->stall_us = getenv("MTCP_GPU_STALL_US") ? (uint32_t)atol(getenv("MTCP_GPU_STALL_US")) : 0;
     /* MTCP_GPU_TX_STALL_AFTER=k: the (k+1)-th tx fill waits MTCP_GPU_STALL_US
-     * behind mtcp_gpu_debug_stall_host (the bounded send_pkts) */
+     * behind mtcp_gpu_debug_stall (the bounded send_pkts) */
     g->tx_stall_after = getenv("MTCP_GPU_TX_STALL_AFTER") ? atol(getenv("MTCP_GPU_TX_STALL_AFTER")) : -1;
 #endif
     g->wait_us = gpu_wait_us();
@@ -383,7 +414,8 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 
     ndev = mtcp_gpu_device_count();
     dev = ndev > 0 ? gpu_pick_device(ctx->cpu, ndev) : -1;
-    if (dev >= 0 && !gpu_thread_admit(dev)) {
+    place = dev >= 0 ? gpu_thread_admit(dev) : 0;
+    if (dev >= 0 && !place) {
         /* said once per refused thread, at init: a deployment with more
          * threads than the limit per GPU sees where its offload went */
         TRACE_CONFIG("gpu_module: core %d: GPU %d already serves %d mTCP threads "
@@ -393,9 +425,16 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
         g->passthrough = 1;                  /* mTCP's own checksums on this core */
         return;
     }
+    if (dev >= 0 && gpu_queues_shared(place))
+        TRACE_CONFIG("gpu_module: core %d: offloading thread %d on GPU %d needs more than the "
+                     "%d hardware queues of GPU_MAX_HW_QUEUES: its stream shares a queue with "
+                     "another thread's, whose stalled GPU work can then delay it\n",
+                     ctx->cpu, place, dev, gpu_hw_queues());
     g->slot_dev = dev;
-    /* compact 16 B records: the rxqs read the verdict only (40 -> 16 B of D2H per frame) */
+    /* compact 16 B records: the rxqs read the verdict only (40 -> 16 B of D2H per frame);
+     * every wait of the context (and of its rxqs) bounded by MTCP_GPU_WAIT_TIMEOUT_MS */
     if (dev < 0 || mtcp_gpu_open(&g->gpu, dev, NULL, 1, MTCP_GPU_F_COMPACT) != MTCP_GPU_OK ||
+        mtcp_gpu_set_wait_limit(g->gpu, g->wait_us) != MTCP_GPU_OK ||
         mtcp_gpu_reserve(g->gpu, 0, 0) != MTCP_GPU_OK) {     /* load the kernels now */
         if (g->gpu)
             mtcp_gpu_close(g->gpu);
@@ -466,7 +505,7 @@ static void gpu_tx_flush(struct gpu_private_context *g, int nif)
     if (g->gpu) {
 #ifdef MTCP_GPU_TESTING
         if (g->tx_fills == g->tx_stall_after)
-            (void)mtcp_gpu_debug_stall_host(g->gpu, g->stall_us);
+            (void)mtcp_gpu_debug_stall(g->gpu, g->stall_us);
 #endif
         g->tx_fills++;
         rc = mtcp_gpu_tx_fill_ptrs_for(g->gpu, t->pkt, t->len, t->n, NULL, g->wait_us);

@@ -47,6 +47,7 @@ int main(void)
     struct gpu_private_context gs[16];
     int def16, def_other_dev, after_release, all16, zero, three;
     unsigned long long w_default, w_zero, w_neg, w_big, w_5000;
+    int q_default_2, q_4, q_5, q_env8_5, q_env8_9;
 
     unsetenv("MTCP_GPU_THREADS");
     def16 = admit_n(0, 16, gs);              /* default: 2 of 16 on device 0 */
@@ -67,6 +68,16 @@ int main(void)
     three = admit_n(0, 16, gs);
     release_all(gs, 16);
 
+    /* hardware queues: one stream per offloading thread against GPU_MAX_HW_QUEUES */
+    unsetenv("GPU_MAX_HW_QUEUES");
+    q_default_2 = gpu_queues_shared(2);
+    q_4 = gpu_queues_shared(4);
+    q_5 = gpu_queues_shared(5);
+    setenv("GPU_MAX_HW_QUEUES", "8", 1);
+    q_env8_5 = gpu_queues_shared(5);
+    q_env8_9 = gpu_queues_shared(9);
+    unsetenv("GPU_MAX_HW_QUEUES");
+
     unsetenv("MTCP_GPU_WAIT_TIMEOUT_MS");
     w_default = gpu_wait_us();
     setenv("MTCP_GPU_WAIT_TIMEOUT_MS", "0", 1);
@@ -81,8 +92,9 @@ int main(void)
     printf("{\"default_of_16\": %d, \"default_other_device_of_4\": %d, \"after_release_of_3\": %d, "
            "\"all_of_16\": %d, \"zero_of_16\": %d, \"three_of_16\": %d, \"count_left\": %d, "
            "\"wait_default\": %llu, \"wait_zero\": %llu, \"wait_negative\": %llu, "
-           "\"wait_5000000ms\": %llu, \"wait_5000ms\": %llu}\n",
+           "\"wait_5000000ms\": %llu, \"wait_5000ms\": %llu, "
+           "\"queues_shared\": [%d, %d, %d, %d, %d]}\n",
            def16, def_other_dev, after_release, all16, zero, three, gpu_thread_count[0],
-           w_default, w_zero, w_neg, w_big, w_5000);
+           w_default, w_zero, w_neg, w_big, w_5000, q_default_2, q_4, q_5, q_env8_5, q_env8_9);
     return 0;
 }

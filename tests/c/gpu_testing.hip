@@ -1,6 +1,6 @@
 // gpu_testing.hip — TEST-ONLY library (tests/c/libmtcp_gpu_testing.so): the
 // fault injection the hang tests use (tests/c/mtcp_gpu_testing.h), built on
-// the product's public ABI only (mtcp_gpu_stream, mtcp_gpu_host_stream), so that the product
+// the product's public ABI only (mtcp_gpu_stream), so that the product
 // library exports no debug entry point.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,7 +36,6 @@ extern "C" int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us) {
     return stall_on(reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx)), us);
 }
 
-extern "C" int mtcp_gpu_debug_stall_host(mtcp_gpu_ctx *ctx, uint32_t us) {
-    if (!ctx) return MTCP_GPU_EINVAL;
-    return stall_on(reinterpret_cast<hipStream_t>(mtcp_gpu_host_stream(ctx)), us);
+extern "C" int mtcp_gpu_debug_stall_stream(void *stream, uint32_t us) {
+    return stall_on(reinterpret_cast<hipStream_t>(stream), us);
 }

@@ -16,15 +16,15 @@ extern "C" {
 #endif
 
 /* Fault injection for tests of a caller's hang handling: queue a kernel on
- * the context's stream (mtcp_gpu_stream) that keeps it busy for `us`
- * microseconds (at most 10 s), so that work queued behind it completes that
- * much later.  MTCP_GPU_EINVAL for a NULL context or a longer stall. */
+ * the context's stream (mtcp_gpu_stream: its host calls, tx fills and rxqs
+ * all run there) that keeps it busy for `us` microseconds (at most 10 s), so
+ * that work queued behind it completes that much later.  MTCP_GPU_EINVAL for
+ * a NULL context or a longer stall. */
 int mtcp_gpu_debug_stall(mtcp_gpu_ctx *ctx, uint32_t us);
 
-/* The same on the stream of the context's host-memory calls
- * (mtcp_gpu_host_stream): the next mtcp_gpu_tx_fill_ptrs[_for] completes
- * `us` later (the bounded tx fill of gpu_module.c is tested with it). */
-int mtcp_gpu_debug_stall_host(mtcp_gpu_ctx *ctx, uint32_t us);
+/* The same on any stream of the caller's (a hipStream_t, as void*; not
+ * NULL): the close test stalls a caller stream with a launch queued behind. */
+int mtcp_gpu_debug_stall_stream(void *stream, uint32_t us);
 
 #ifdef __cplusplus
 }

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == set(_lib.EXPORTS), decl ^ set(_lib.EXPORTS)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mtcp_gpu_abi_version() == 4
+    assert lib.mtcp_gpu_abi_version() == 5
     assert lib.mtcp_gpu_strerror(-22) == b"invalid argument"
 
 

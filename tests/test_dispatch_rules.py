@@ -132,3 +132,17 @@ def test_rules_invariants(choose):
                   (1 << 16, 64, 0, 0, 1, 0, AUTO, 0)])
     assert got == ["rx_kernel<unrolled>", "rx_kernel<unrolled>", "rx_kernel<unrolled,line-aligned>",
                    "rx_kernel<sorted>", "rx_group_kernel<quad>"]
+
+
+def test_small_hinted_batches_keep_the_wave_kernel(choose):
+    """a hinted batch of at most 2 048 frames with 256-320 B slots
+    (a small io_module aggregate) takes the wave kernel as the same batch
+    without a hint does; the quad rule starts above 2 048 frames, where the
+    dispatch map measured it."""
+    for n in (1, 64, 512, 2048):
+        for s in (200, 256, 300):
+            sl = (s + 63) & ~63
+            hinted, plain = choose([(n, sl, s, s, 1, 0, AUTO, 0), (n, sl, 0, 0, 1, 0, AUTO, 0)])
+            assert hinted == plain and hinted.startswith("rx_wave_kernel"), (n, s, hinted, plain)
+    got = choose([(4096, 256, 256, 256, 1, 0, AUTO, 0)])
+    assert got[0].startswith("rx_group_kernel<oct>"), got

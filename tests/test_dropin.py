@@ -310,7 +310,7 @@ def test_dropin_tx_gpu_hang_falls_back_to_mtcp(tmp_path):
     """The tx fill never blocks mTCP's main loop on a GPU that stops
     answering (mTCP's own fill never waits on a device: tcp_out.c:320-329,
     ip_out.c:147-165, run from core.c:818-824).  The third send_pkts' fill
-    waits 1.5 s on the GPU behind mtcp_gpu_debug_stall_host; gpu_module's
+    waits 1.5 s on the GPU behind mtcp_gpu_debug_stall; gpu_module's
     wait gives up after MTCP_GPU_WAIT_TIMEOUT_MS (100 ms), fills those frames
     with mTCP's ip_fast_csum / TCPCalcChecksum, abandons the GPU, and answers
     dev_ioctl -1 from then on, so mTCP fills the rest itself.  Every

@@ -289,6 +289,9 @@ def test_admission_default_and_limits():
     assert (r["all_of_16"], r["zero_of_16"], r["three_of_16"], r["count_left"]) == (16, 0, 3, 0)
     assert (r["wait_default"], r["wait_zero"], r["wait_negative"]) == (2000000, 0, 0)
     assert r["wait_5000000ms"] == 4294967000 and r["wait_5000ms"] == 5000000
+    # one stream per offloading thread: the default two threads, and up to
+    # four, never share a hardware queue (GPU_MAX_HW_QUEUES, 4 by default)
+    assert r["queues_shared"] == [0, 0, 1, 0, 1]
 
 
 def test_production_build_has_no_fault_injection(tmp_path):

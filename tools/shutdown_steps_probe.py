@@ -44,12 +44,12 @@ def main():
         # test_tx_fill_ptrs_for_gives_up_and_abandons first: a tx fill that
         # times out behind an 800 ms host-stream stall, the context abandoned
         from mtcp_amd._lib import MtcpGpuError
-        T.mtcp_gpu_debug_stall_host.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        T.mtcp_gpu_debug_stall.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         offs = g.desc[:64]["offset"].astype("int64")
         z = gpu.Context(0)
         host = g.buf.copy()
         z.tx_fill_ptrs(host, offs, g.desc[:64]["len"], timeout_us=2_000_000)
-        assert T.mtcp_gpu_debug_stall_host(z._h, 800 * 1000) == 0
+        assert T.mtcp_gpu_debug_stall(z._h, 800 * 1000) == 0
         try:
             z.tx_fill_ptrs(host, offs, g.desc[:64]["len"], timeout_us=30_000)
         except MtcpGpuError:
