@@ -75,7 +75,9 @@ def main():
     L = lib()
     T = ctypes.CDLL(os.path.join(ROOT, "tests", "c", "libmtcp_gpu_testing.so"))
     T.mtcp_gpu_debug_stall.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-    hip = ctypes.CDLL("libamdhip64.so")
+    # the HIP runtime libmtcp_gpu.so loaded (its path from this process's maps)
+    hip_path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+    hip = ctypes.CDLL(hip_path)
     hip.hipStreamQuery.argtypes = [ctypes.c_void_p]
     g = load_golden()
     part = g.desc[:AGG]

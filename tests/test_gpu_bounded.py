@@ -47,7 +47,7 @@ def gpu():
     return g
 
 
-def testing_lib():
+def stall_lib():
     T = ctypes.CDLL(os.path.join(ROOT, "tests", "c", "libmtcp_gpu_testing.so"))
     T.mtcp_gpu_debug_stall.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     T.mtcp_gpu_debug_stall.restype = ctypes.c_int
@@ -147,7 +147,7 @@ def case_flow_hash(L, ctx, golden):
 def case_addr_pool(L, ctx, golden):
     from mtcp_amd._types import ADDR_ENTRY_DTYPE
     args = (1, 4, 0x0A00000A, 4, 0x0B00000A, 0x5000, 1)       # core, nq, saddr, num_addr, daddr, dport, endian
-    out = np.full(4 * 64511, SENTINEL, np.uint8).view(ADDR_ENTRY_DTYPE)
+    out = np.full(4 * 64511 * ADDR_ENTRY_DTYPE.itemsize, SENTINEL, np.uint8).view(ADDR_ENTRY_DTYPE)
     found = ctypes.c_uint32(0xFFFF)
     rc = L.mtcp_gpu_addr_pool_search(ctx._h, *args, out.ctypes.data, len(out), ctypes.byref(found))
     want = oracle.addr_pool_search(None, *args)
@@ -209,7 +209,7 @@ def test_each_host_call_gives_up_at_the_limit(gpu, golden, name):
     them); the context is abandoned (EIO, no device call); closing it does
     not wait; a fresh context gives the reference's results."""
     from mtcp_amd._lib import lib
-    L, T = lib(), testing_lib()
+    L, T = lib(), stall_lib()
     ctx = gpu.Context(0, rss=True, rss_queues=golden.rss_num_queues)
     handle = ctx.stream
     rc, _, check = CASES[name](L, ctx, golden)             # unbounded: stages sized, kernels loaded
@@ -244,7 +244,7 @@ def test_bounded_pipeline_gives_up_mid_call(gpu):
     stages (stage 0 waits behind the stall): ETIMEDOUT, and not one record
     of the batches that did run is written into the caller's results."""
     from mtcp_amd._lib import lib
-    L, T = lib(), testing_lib()
+    L, T = lib(), stall_lib()
     n, seed = 150000, 53
     desc, nbytes = pktgen.layout(n, 1500, 6, seed)
     host = np.zeros(nbytes, np.uint8)
@@ -270,7 +270,7 @@ def test_sync_times_out_without_abandoning(gpu, golden):
     work): after the stall, sync succeeds and a host call gives the
     reference's results on the same context."""
     from mtcp_amd._lib import lib
-    L, T = lib(), testing_lib()
+    L, T = lib(), stall_lib()
     with gpu.Context(0, rss=True, rss_queues=golden.rss_num_queues) as ctx:
         ctx.wait_limit = LIMIT_US
         assert T.mtcp_gpu_debug_stall(ctx._h, 300_000) == 0
@@ -292,7 +292,7 @@ def test_reserve_and_rxq_calls_are_bounded(gpu, golden):
     context's limit) answers ETIMEDOUT, serves no verdicts, and the rxq's
     destroy returns without waiting for the stall."""
     from mtcp_amd._lib import lib
-    L, T = lib(), testing_lib()
+    L, T = lib(), stall_lib()
     a = gpu.Context(0)
     ha = a.stream
     a.wait_limit = LIMIT_US
@@ -330,7 +330,7 @@ def test_close_with_a_caller_stream_launch_pending(gpu):
     context with a different RSS key is opened and used meanwhile.  The
     pending launch still computes with its own key: the device-side tables
     are shared per key and never freed or rewritten (rss_tables_for)."""
-    T = testing_lib()
+    T = stall_lib()
     n, seed = 4096, 59
     desc, nbytes = pktgen.layout(n, "bimodal", 6, seed)
     buf = np.zeros(nbytes, np.uint8)
