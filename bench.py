@@ -252,6 +252,40 @@ def read_ceiling(d_buf, nbytes, stream, reps=20):
     return float(us.value), int(shape.value)
 
 
+def gpu_identity(device: int) -> dict:
+    """The GPU a rank runs on: its PCI address and NUMA node (sysfs), so that
+    an N-GPU line shows N distinct GPUs and where each sits."""
+    from mtcp_amd import gpu
+    bdf = gpu.device_pci_bus_id(device)
+    try:
+        node = int(open(os.path.join("/sys/bus/pci/devices", bdf, "numa_node")).read().strip())
+    except (OSError, ValueError):
+        node = -1
+    return {"gpu_pci": bdf, "numa_node": node}
+
+
+def rank_summary(per_rank: list, forced_device) -> dict:
+    """What the N ranks' own measurements say, for roofline: each rank's GPU
+    (pci, node), its event-timed launch and wall time, its own read ceiling
+    and the kernel's fraction of it; the spread of the launch times (max /
+    min); and how many distinct GPUs the ranks ran on.  Fewer GPUs than ranks
+    without MTCP_BENCH_DEVICE (a launcher that mapped two ranks to one GPU)
+    is flagged, so such a line cannot pass for an N-GPU number."""
+    kern = [r["kern_ms"] for r in per_rank]
+    distinct = len({r["gpu_pci"] for r in per_rank})
+    out = {"per_rank": sorted(per_rank, key=lambda r: r["rank"]),
+           "kern_ms_spread": round(max(kern) / min(kern), 4) if min(kern) > 0 else None,
+           "distinct_gpus": distinct}
+    if distinct < len(per_rank):
+        if forced_device is not None:
+            out["note"] = (f"MTCP_BENCH_DEVICE={forced_device}: every rank on one device (a rehearsal "
+                           f"of the N-rank path; the timings are not an N-GPU measurement)")
+        else:
+            out["warning"] = (f"{len(per_rank)} ranks ran on {distinct} distinct GPU(s): ranks shared a GPU, "
+                              f"this is not a {len(per_rank)}-GPU measurement")
+    return out
+
+
 def patch_ceiling(d_buf, d_desc, n, stream, reps=20):
     """The f1 row's ceiling, measured now on its own frames: the tx fill's
     access pattern without its arithmetic (read every frame, write the two
@@ -825,7 +859,7 @@ def main():
     step_rcs = []
     step = lambda: step_rcs.append(rx_fn(*rx_args))
 
-    ceiling = None
+    ceiling = my_ceiling_us = None
     if args.ceiling == "on":
         # The box's read ceiling on this rank's own frame buffer, measured
         # right before the kernel so that both see the same device state
@@ -838,6 +872,7 @@ def main():
             ceiling = read_ceiling(d_buf, sh.nbytes, stream)
         except Exception as exc:   # never costs the headline line
             ceiling = repr(exc)
+        my_ceiling_us = ceiling[0] if isinstance(ceiling, tuple) else None
         if world > 1:
             t = torch.tensor([ceiling[0] if isinstance(ceiling, tuple) else -1.0], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -892,7 +927,16 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
+    # this rank's own view (roofline.per_rank): which GPU, its launches, its
+    # wall time and its own read ceiling
+    mine = dict(rank=rank, device=device, **gpu_identity(device), kern_ms=round(kern_ms, 5),
+                wall_ms=round(elapsed * 1e3, 3),
+                read_ceiling_us=round(my_ceiling_us, 2) if my_ceiling_us else None,
+                kernel_frac_of_ceiling=round(my_ceiling_us / (kern_ms * 1e3), 4) if my_ceiling_us else None)
+    per_rank = [mine]
     if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
@@ -1009,6 +1053,11 @@ def main():
                     "note": "each rank's seconds from its start to the end of its legs and its peak "
                             "resident host memory, the max over ranks"},
         }
+        ranks = rank_summary(per_rank, os.environ.get("MTCP_BENCH_DEVICE"))
+        for k in ("note", "warning"):
+            if k in ranks:
+                line["config"][k] = ranks.pop(k)
+        line["roofline"].update(ranks)
         if isinstance(ceiling, tuple):
             cus, shape = ceiling
             line["roofline"]["read_ceiling"] = {

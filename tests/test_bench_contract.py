@@ -153,3 +153,30 @@ def test_read_ceiling_probe_is_built_and_exported(bench, monkeypatch):
     monkeypatch.setattr("sys.argv", ["bench.py"])
     a = bench.parse()
     assert (a.ceiling, a.numa) == ("on", "on")
+
+
+def _rank(r, pci, kern, node=0):
+    return {"rank": r, "device": r, "gpu_pci": pci, "numa_node": node, "kern_ms": kern, "wall_ms": 10.0,
+            "read_ceiling_us": 220.0, "kernel_frac_of_ceiling": round(0.22 / kern, 4)}
+
+
+def test_rank_summary_shape(bench):
+    """the N > 1 line carries every rank's GPU (pci,
+    NUMA node), event-timed launch, wall time and own read ceiling, the
+    launch spread and the number of distinct GPUs; ranks sharing a GPU are
+    flagged unless MTCP_BENCH_DEVICE forced it (then a note says so)."""
+    eight = [_rank(r, f"0000:{0x10 * (r + 1):02x}:00.0", 0.24 + 0.001 * r, r // 4) for r in reversed(range(8))]
+    s = bench.rank_summary(eight, None)
+    assert [r["rank"] for r in s["per_rank"]] == list(range(8))
+    assert set(s["per_rank"][0]) == {"rank", "device", "gpu_pci", "numa_node", "kern_ms", "wall_ms",
+                                     "read_ceiling_us", "kernel_frac_of_ceiling"}
+    assert s["distinct_gpus"] == 8 and "warning" not in s and "note" not in s
+    assert s["kern_ms_spread"] == round(0.247 / 0.24, 4)
+    shared = [_rank(r, "0000:10:00.0" if r < 2 else f"0000:{0x10 * (r + 1):02x}:00.0", 0.24) for r in range(8)]
+    s = bench.rank_summary(shared, None)
+    assert s["distinct_gpus"] == 7 and "7 distinct" in s["warning"] and "not a 8-GPU" in s["warning"]
+    one = [_rank(r, "0000:10:00.0", 0.24) for r in range(8)]
+    s = bench.rank_summary(one, "0")
+    assert s["distinct_gpus"] == 1 and "warning" not in s and s["note"].startswith("MTCP_BENCH_DEVICE=0")
+    s = bench.rank_summary([_rank(0, "0000:10:00.0", 0.24)], None)
+    assert s["distinct_gpus"] == 1 and s["kern_ms_spread"] == 1.0 and "warning" not in s

@@ -198,3 +198,10 @@ def test_bench_driver_form_eight_ranks_on_one_device(gpu):
     assert line["pcie_inclusive"]["n_gpus"] == 8 and line["pcie_inclusive"]["value"] > 0
     assert "c4_per_gpu" not in line
     assert line["run"]["wall_s_max_rank"] > 0
+    # every rank's own view: all eight on the one device
+    ro = line["roofline"]
+    assert [r["rank"] for r in ro["per_rank"]] == list(range(8))
+    assert all(r["device"] == 0 and r["kern_ms"] > 0 and r["wall_ms"] > 0 for r in ro["per_rank"])
+    assert len({r["gpu_pci"] for r in ro["per_rank"]}) == 1 == ro["distinct_gpus"]
+    assert ro["kern_ms_spread"] >= 1.0
+    assert line["config"]["note"].startswith("MTCP_BENCH_DEVICE=0") and "warning" not in line["config"]
