@@ -76,8 +76,10 @@
  * their frames itself (dev_ioctl -1), as dpdk_module.c claims an offload
  * only where the device has it (dpdk_module.c:809-816): past two threads a
  * GPU's PCIe link is full and an offloading thread waits on it while its
- * core could check the frames.  MTCP_GPU_THREADS=k sets
- * another limit, MTCP_GPU_THREADS=all admits every thread.
+ * core could check the frames; where 8 or more mTCP threads
+ * share a GPU (mtcp.conf's num_cores over the GPUs) none offloads by
+ * default.  MTCP_GPU_THREADS=k sets another limit, MTCP_GPU_THREADS=all
+ * admits every thread.
  *
  * Fault injection (MTCP_GPU_FAIL_AFTER, MTCP_GPU_STALL_AFTER /
  * MTCP_GPU_TX_STALL_AFTER / MTCP_GPU_STALL_US) exists only in test builds (-DMTCP_GPU_TESTING, linked
@@ -119,6 +121,8 @@
 #define GPU_FRAME_JUMBO 9216ull           /* the largest frame a burst is expected to bring */
 #define GPU_TX_MAX     4096               /* frames recorded between two send_pkts */
 #define GPU_THREADS_DEFAULT 2             /* offloading threads per GPU */
+#define GPU_CROWDED_THREADS 8             /* mTCP threads per GPU from which, by default,
+                                             none offloads */
 #define GPU_STREAMS_PER_THREAD 1          /* a thread's GPU context runs its rx aggregates and
                                              tx fills on its one stream (include/mtcp_gpu.h) */
 
@@ -302,16 +306,28 @@ static int gpu_pick_device(int cpu, int ndev)
  * wrapped backend alone (dev_ioctl -1: mTCP's own checksums).  One GPU's
  * PCIe link carries the frames of about two threads, so
  * threads beyond that would wait on the link while their cores could check
- * frames themselves.  k = GPU_THREADS_DEFAULT unless MTCP_GPU_THREADS says
- * otherwise ("all": no limit).  A thread holds its slot from a successful
- * open until destroy_handle (gpu_thread_release). */
+ * frames themselves.  k = GPU_THREADS_DEFAULT, except where a GPU is shared
+ * by GPU_CROWDED_THREADS or more mTCP threads (CONFIG.num_cores, mtcp.h:147,
+ * over the GPUs): there an offloading thread runs no faster than a thread
+ * checking its own frames (8 and 16 threads: offloading and software threads
+ * at the same per-thread rate) and its frames cost the host
+ * two more passes over memory (the copy into pinned staging and the DMA
+ * read), so by default none offloads.  MTCP_GPU_THREADS=k sets the limit
+ * ("all": no limit).  A thread holds its slot from a successful open until
+ * destroy_handle (gpu_thread_release). */
 static int gpu_thread_count[GPU_TOPO_MAX_DEVS];
 
-static int gpu_thread_limit(void)
+/* mTCP threads per GPU in this process (0: unknown) */
+static int gpu_threads_per_gpu(int ndev)
+{
+    return ndev > 0 && CONFIG.num_cores > 0 ? (CONFIG.num_cores + ndev - 1) / ndev : 0;
+}
+
+static int gpu_thread_limit(int per_gpu)
 {
     const char *lim = getenv("MTCP_GPU_THREADS");
     if (!lim || !*lim)
-        return GPU_THREADS_DEFAULT;
+        return per_gpu >= GPU_CROWDED_THREADS ? 0 : GPU_THREADS_DEFAULT;
     if (strcmp(lim, "all") == 0)
         return -1;
     return atoi(lim) < 0 ? 0 : atoi(lim);
@@ -319,9 +335,9 @@ static int gpu_thread_limit(void)
 
 /* Returns the thread's place among the device's offloading threads (1, 2,
  * ...), or 0 when it is refused. */
-static int gpu_thread_admit(int dev)
+static int gpu_thread_admit(int dev, int per_gpu)
 {
-    const int lim = gpu_thread_limit();         /* -1: no limit (still counted) */
+    const int lim = gpu_thread_limit(per_gpu);  /* -1: no limit (still counted) */
     int n;
     if (dev < 0 || dev >= GPU_TOPO_MAX_DEVS)
         return 1;
@@ -375,7 +391,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
     struct gpu_private_context *g = calloc(1, sizeof(*g));
     const char *pl = getenv("MTCP_GPU_PIPELINE");
     const char *tx = getenv("MTCP_GPU_TX");
-    int ndev, dev, place, i;
+    int ndev, dev, place, per_gpu, i;
 
     gpu_inner_module->init_handle(ctx);       /* sets ctx->io_private_context */
     if (!g) {
@@ -414,14 +430,21 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 
     ndev = mtcp_gpu_device_count();
     dev = ndev > 0 ? gpu_pick_device(ctx->cpu, ndev) : -1;
-    place = dev >= 0 ? gpu_thread_admit(dev) : 0;
+    per_gpu = gpu_threads_per_gpu(ndev);
+    place = dev >= 0 ? gpu_thread_admit(dev, per_gpu) : 0;
     if (dev >= 0 && !place) {
         /* said once per refused thread, at init: a deployment with more
          * threads than the limit per GPU sees where its offload went */
-        TRACE_CONFIG("gpu_module: core %d: GPU %d already serves %d mTCP threads "
-                     "(MTCP_GPU_THREADS, default %d); this thread checks its own frames "
-                     "(MTCP_GPU_THREADS=all offloads every thread)\n",
-                     ctx->cpu, dev, gpu_thread_limit(), GPU_THREADS_DEFAULT);
+        if (gpu_thread_limit(per_gpu) == 0 && !getenv("MTCP_GPU_THREADS"))
+            TRACE_CONFIG("gpu_module: core %d: %d mTCP threads share each GPU (>= %d): by default "
+                         "none offloads and this thread checks its own frames "
+                         "(MTCP_GPU_THREADS=k offloads k threads per GPU)\n",
+                         ctx->cpu, per_gpu, GPU_CROWDED_THREADS);
+        else
+            TRACE_CONFIG("gpu_module: core %d: GPU %d already serves %d mTCP threads "
+                         "(MTCP_GPU_THREADS, default %d); this thread checks its own frames "
+                         "(MTCP_GPU_THREADS=all offloads every thread)\n",
+                         ctx->cpu, dev, gpu_thread_limit(per_gpu), GPU_THREADS_DEFAULT);
         g->passthrough = 1;                  /* mTCP's own checksums on this core */
         return;
     }

@@ -69,7 +69,7 @@ uint16_t TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t d
 
 extern io_module_func gpu_module_func;
 int gpu_module_thread_device(struct mtcp_thread_context *ctx);   /* test build of gpu_module.c */
-struct mtcp_config CONFIG = {1};                   /* one interface (mtcp.conf's port list) */
+struct mtcp_config CONFIG = {1, 1};                /* one interface (mtcp.conf's port list); num_cores set below */
 extern io_module_func *gpu_inner_module;
 
 /* RXLOOP_REF: the reference's rx chain (ref_glue.h's ref_rx_packet) */
@@ -351,6 +351,7 @@ int main(int argc, char **argv)
     uint8_t *tx_buf = NULL;
     threads = argc > 5 ? atoi(argv[5]) : 1;
     if (threads < 1 || threads > 64) { fprintf(stderr, "THREADS: 1..64\n"); return 1; }
+    CONFIG.num_cores = threads;                     /* mtcp.conf's num_cores: one mTCP thread each */
     buf = slurp(argv[1], &nb);
     desc = slurp(argv[2], &nd);
     n = (uint32_t)(nd / sizeof(mtcp_gpu_desc));

@@ -170,6 +170,24 @@ def test_gpu_threads_limit_splits_the_checks(tmp_path, golden, limit):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("limit,want", [(None, 0), ("2", 2)])
+def test_crowded_gpu_offloads_none_by_default(tmp_path, golden, limit, want):
+    """Eight mTCP threads on the one GPU (num_cores 8): by default none
+    offloads (an offloading thread runs no faster than a software one there,
+    DESIGN.md §5), MTCP_GPU_THREADS=2 still offloads two; either way every
+    thread drops exactly the frames mTCP's own checks drop."""
+    env = {"MTCP_GPU_THREADS": limit} if limit is not None else {}
+    if limit is None:
+        os.environ.pop("MTCP_GPU_THREADS", None)
+    stats, status = run_rxloop(tmp_path, threads=8, mode="timing", env=env)
+    drop = rx_drops(golden)
+    assert stats["offloading_threads"] == want
+    assert stats["seen"] == stats["frames"] == len(golden.desc)
+    assert np.array_equal(status == 0, drop)
+    assert stats["rx_errors"] == int(drop.sum())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("threads", [1, 4])
 def test_gpu_module_fills_tx_checksums(tmp_path, golden, threads):
     """MTCP_GPU_TX=1: dev_ioctl(PKT_TX_TCPIP_CSUM_PEEK) answers 0, mTCP leaves
@@ -292,6 +310,12 @@ def test_admission_default_and_limits():
     # one stream per offloading thread: the default two threads, and up to
     # four, never share a hardware queue (GPU_MAX_HW_QUEUES, 4 by default)
     assert r["queues_shared"] == [0, 0, 1, 0, 1]
+    # crowded GPUs: 16 threads on one GPU offload none by
+    # default, 16 threads over 8 GPUs keep two per GPU, 7 keep two, 8 none;
+    # an explicit MTCP_GPU_THREADS still decides
+    c = r["crowded"]
+    assert (c["16_on_1"], c["16_on_8"], c["7_on_1"], c["8_on_1"], c["16_on_1_k1"]) == (0, 2, 2, 0, 1)
+    assert (c["per_gpu_16_8"], c["per_gpu_17_8"]) == (2, 3)
 
 
 def test_production_build_has_no_fault_injection(tmp_path):
