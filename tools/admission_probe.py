@@ -11,6 +11,7 @@ the box's CPU quota throttled the process meanwhile (cgroup cpu.stat), so a
 slow run can be told apart from a throttled one.
 
   python tools/admission_probe.py [reps] > gpurun_out/admission.jsonl
+  (ADM_THREADS=1,2,4,8,16: other thread counts)
 """
 import json
 import os
@@ -47,6 +48,9 @@ def cpu_stat(d):
     return out
 
 
+THREADS = tuple(int(t) for t in os.environ.get("ADM_THREADS", "8,12,16").split(","))
+
+
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 6
     n = 1 << 18
@@ -66,7 +70,7 @@ def main():
     limits = ("default", "1", "0")
     with tempfile.TemporaryDirectory() as tmp:
         for rep in range(reps):
-            for threads in (8, 12, 16):
+            for threads in THREADS:
                 order = limits[rep % 3:] + limits[:rep % 3]
                 for limit in order:
                     os.environ["RXLOOP_PASSES"] = str(4 * threads)
