@@ -76,7 +76,7 @@
  * their frames itself (dev_ioctl -1), as dpdk_module.c claims an offload
  * only where the device has it (dpdk_module.c:809-816): past two threads a
  * GPU's PCIe link is full and an offloading thread waits on it while its
- * core could check the frames; where 8 or more mTCP threads
+ * core could check the frames; where 4 or more mTCP threads
  * share a GPU (mtcp.conf's num_cores over the GPUs) none offloads by
  * default.  MTCP_GPU_THREADS=k sets another limit, MTCP_GPU_THREADS=all
  * admits every thread.
@@ -121,7 +121,7 @@
 #define GPU_FRAME_JUMBO 9216ull           /* the largest frame a burst is expected to bring */
 #define GPU_TX_MAX     4096               /* frames recorded between two send_pkts */
 #define GPU_THREADS_DEFAULT 2             /* offloading threads per GPU */
-#define GPU_CROWDED_THREADS 8             /* mTCP threads per GPU from which, by default,
+#define GPU_CROWDED_THREADS 4             /* mTCP threads per GPU from which, by default,
                                              none offloads */
 #define GPU_STREAMS_PER_THREAD 1          /* a thread's GPU context runs its rx aggregates and
                                              tx fills on its one stream (include/mtcp_gpu.h) */
@@ -307,12 +307,14 @@ static int gpu_pick_device(int cpu, int ndev)
  * PCIe link carries the frames of about two threads, so
  * threads beyond that would wait on the link while their cores could check
  * frames themselves.  k = GPU_THREADS_DEFAULT, except where a GPU is shared
- * by GPU_CROWDED_THREADS or more mTCP threads (CONFIG.num_cores, mtcp.h:147,
- * over the GPUs): there an offloading thread runs no faster than a thread
- * checking its own frames (8 and 16 threads: offloading and software threads
- * at the same per-thread rate) and its frames cost the host
- * two more passes over memory (the copy into pinned staging and the DMA
- * read), so by default none offloads.  MTCP_GPU_THREADS=k sets the limit
+ * by GPU_CROWDED_THREADS (4) or more mTCP threads (CONFIG.num_cores,
+ * mtcp.h:147, over the GPUs): there an offloading thread runs no faster than
+ * a thread checking its own frames (from 4 threads on, offloading and
+ * software threads at the same per-thread rate and the default at 0.92-1.00
+ * of no offload in three rounds of paired runs) and its
+ * frames cost the host two more passes over memory (the copy into pinned
+ * staging and the DMA read) and more CPU per frame, so by default none
+ * offloads; at 1-3 threads per GPU two offload (1.6-1.9x at 1-2 threads).  MTCP_GPU_THREADS=k sets the limit
  * ("all": no limit).  A thread holds its slot from a successful open until
  * destroy_handle (gpu_thread_release). */
 static int gpu_thread_count[GPU_TOPO_MAX_DEVS];

@@ -5,7 +5,7 @@
  *   admit_test  -> one JSON line of results; tests/test_io_module.py checks it
  *
  * Admission: at most GPU_THREADS_DEFAULT (2) mTCP threads per GPU offload
- * (none where 8 or more mTCP threads share a GPU) unless MTCP_GPU_THREADS
+ * (none where 4 or more mTCP threads share a GPU) unless MTCP_GPU_THREADS
  * says otherwise ("all": every thread); a thread's
  * slot is given back when its context fails to open or is destroyed.
  * MTCP_GPU_WAIT_TIMEOUT_MS: default 2000 ms, <= 0 no limit, clamped to the
@@ -51,7 +51,8 @@ int main(void)
     int def16, def_other_dev, after_release, all16, zero, three;
     unsigned long long w_default, w_zero, w_neg, w_big, w_5000;
     int q_default_2, q_4, q_5, q_env8_5, q_env8_9;
-    int crowd_16_on_1, crowd_16_on_8, crowd_7_on_1, crowd_8_on_1, crowd_16_on_1_k1, per_gpu_16_8, per_gpu_17_8;
+    int crowd_16_on_1, crowd_16_on_8, crowd_3_on_1, crowd_4_on_1, crowd_16_on_1_k1, crowd_24_on_8;
+    int per_gpu_16_8, per_gpu_17_8;
 
     unsetenv("MTCP_GPU_THREADS");
     def16 = admit_n(0, 16, gs);              /* default: 2 of 16 on device 0 */
@@ -72,7 +73,7 @@ int main(void)
     three = admit_n(0, 16, gs);
     release_all(gs, 16);
 
-    /* crowded GPUs: from 8 mTCP threads per GPU (num_cores over the GPUs)
+    /* crowded GPUs: from 4 mTCP threads per GPU (num_cores over the GPUs)
      * the default admits none; MTCP_GPU_THREADS still decides when set */
     unsetenv("MTCP_GPU_THREADS");
     CONFIG.num_cores = 16;
@@ -82,16 +83,20 @@ int main(void)
     per_gpu_now = per_gpu_16_8 = gpu_threads_per_gpu(8);
     crowd_16_on_8 = admit_n(0, 2, gs);        /* the two threads dealt to one of 8 GPUs */
     release_all(gs, 2);
+    CONFIG.num_cores = 24;
+    per_gpu_now = gpu_threads_per_gpu(8);
+    crowd_24_on_8 = admit_n(0, 3, gs);        /* three threads per GPU still offload two */
+    release_all(gs, 3);
     CONFIG.num_cores = 17;
     per_gpu_17_8 = gpu_threads_per_gpu(8);
-    CONFIG.num_cores = 7;
+    CONFIG.num_cores = 3;
     per_gpu_now = gpu_threads_per_gpu(1);
-    crowd_7_on_1 = admit_n(0, 7, gs);
-    release_all(gs, 7);
-    CONFIG.num_cores = 8;
+    crowd_3_on_1 = admit_n(0, 3, gs);
+    release_all(gs, 3);
+    CONFIG.num_cores = 4;
     per_gpu_now = gpu_threads_per_gpu(1);
-    crowd_8_on_1 = admit_n(0, 8, gs);
-    release_all(gs, 8);
+    crowd_4_on_1 = admit_n(0, 4, gs);
+    release_all(gs, 4);
     setenv("MTCP_GPU_THREADS", "1", 1);
     CONFIG.num_cores = 16;
     per_gpu_now = gpu_threads_per_gpu(1);
@@ -127,10 +132,11 @@ int main(void)
            "\"wait_default\": %llu, \"wait_zero\": %llu, \"wait_negative\": %llu, "
            "\"wait_5000000ms\": %llu, \"wait_5000ms\": %llu, "
            "\"queues_shared\": [%d, %d, %d, %d, %d], "
-           "\"crowded\": {\"16_on_1\": %d, \"16_on_8\": %d, \"7_on_1\": %d, \"8_on_1\": %d, "
-           "\"16_on_1_k1\": %d, \"per_gpu_16_8\": %d, \"per_gpu_17_8\": %d}}\n",
+           "\"crowded\": {\"16_on_1\": %d, \"16_on_8\": %d, \"3_on_1\": %d, \"4_on_1\": %d, "
+           "\"16_on_1_k1\": %d, \"24_on_8\": %d, \"per_gpu_16_8\": %d, \"per_gpu_17_8\": %d}}\n",
            def16, def_other_dev, after_release, all16, zero, three, gpu_thread_count[0],
            w_default, w_zero, w_neg, w_big, w_5000, q_default_2, q_4, q_5, q_env8_5, q_env8_9,
-           crowd_16_on_1, crowd_16_on_8, crowd_7_on_1, crowd_8_on_1, crowd_16_on_1_k1, per_gpu_16_8, per_gpu_17_8);
+           crowd_16_on_1, crowd_16_on_8, crowd_3_on_1, crowd_4_on_1, crowd_16_on_1_k1, crowd_24_on_8,
+           per_gpu_16_8, per_gpu_17_8);
     return 0;
 }

@@ -156,13 +156,13 @@ def test_gpu_threads_limit_splits_the_checks(tmp_path, golden, limit):
     """MTCP_GPU_THREADS=k: k of the four threads offload, the others run on
     the wrapped backend alone and mTCP's own checks run there (the harness's
     timing mode pays for them): every thread drops the same frames.  Unset:
-    the default, two threads per GPU."""
+    the default, none where four threads share the GPU."""
     env = {"MTCP_GPU_THREADS": limit} if limit is not None else {}
     if limit is None:
         os.environ.pop("MTCP_GPU_THREADS", None)
     stats, status = run_rxloop(tmp_path, threads=4, mode="timing", env=env)
     drop = rx_drops(golden)
-    want = {None: 2, "all": 4}[limit] if limit in (None, "all") else int(limit)
+    want = {None: 0, "all": 4}[limit] if limit in (None, "all") else int(limit)
     assert stats["offloading_threads"] == want
     assert stats["seen"] == stats["frames"] == len(golden.desc)
     assert np.array_equal(status == 0, drop)
@@ -170,16 +170,17 @@ def test_gpu_threads_limit_splits_the_checks(tmp_path, golden, limit):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("limit,want", [(None, 0), ("2", 2)])
-def test_crowded_gpu_offloads_none_by_default(tmp_path, golden, limit, want):
-    """Eight mTCP threads on the one GPU (num_cores 8): by default none
-    offloads (an offloading thread runs no faster than a software one there,
-    DESIGN.md §5), MTCP_GPU_THREADS=2 still offloads two; either way every
-    thread drops exactly the frames mTCP's own checks drop."""
+@pytest.mark.parametrize("threads,limit,want", [(3, None, 2), (8, None, 0), (8, "2", 2)])
+def test_crowded_gpu_offloads_none_by_default(tmp_path, golden, threads, limit, want):
+    """Three mTCP threads on the one GPU: two offload by default; eight
+    (num_cores 8): none (from four threads per GPU an offloading thread runs
+    no faster than a software one), and MTCP_GPU_THREADS=2
+    still offloads two; either way every thread drops exactly the frames
+    mTCP's own checks drop."""
     env = {"MTCP_GPU_THREADS": limit} if limit is not None else {}
     if limit is None:
         os.environ.pop("MTCP_GPU_THREADS", None)
-    stats, status = run_rxloop(tmp_path, threads=8, mode="timing", env=env)
+    stats, status = run_rxloop(tmp_path, threads=threads, mode="timing", env=env)
     drop = rx_drops(golden)
     assert stats["offloading_threads"] == want
     assert stats["seen"] == stats["frames"] == len(golden.desc)
@@ -311,10 +312,11 @@ def test_admission_default_and_limits():
     # four, never share a hardware queue (GPU_MAX_HW_QUEUES, 4 by default)
     assert r["queues_shared"] == [0, 0, 1, 0, 1]
     # crowded GPUs: 16 threads on one GPU offload none by
-    # default, 16 threads over 8 GPUs keep two per GPU, 7 keep two, 8 none;
-    # an explicit MTCP_GPU_THREADS still decides
+    # default, 16 (or 24) threads over 8 GPUs keep two per GPU, 3 threads on
+    # one keep two, 4 none; an explicit MTCP_GPU_THREADS still decides
     c = r["crowded"]
-    assert (c["16_on_1"], c["16_on_8"], c["7_on_1"], c["8_on_1"], c["16_on_1_k1"]) == (0, 2, 2, 0, 1)
+    assert (c["16_on_1"], c["16_on_8"], c["3_on_1"], c["4_on_1"], c["16_on_1_k1"], c["24_on_8"]) == \
+        (0, 2, 2, 0, 1, 2)
     assert (c["per_gpu_16_8"], c["per_gpu_17_8"]) == (2, 3)
 
 
