@@ -154,6 +154,10 @@ def parse():
                     help="packets per GPU (default: the config's; tests use smaller batches)")
     ap.add_argument("--dump-records", default=None,
                     help="directory: each rank writes its result records there")
+    ap.add_argument("--prewarm-s", type=float, default=1.0,
+                    help="seconds of untimed launches of the step before the read ceiling and the "
+                         "warmup steps: a box whose GPU sat idle ran its first second 3-4 %% slow, "
+                         "read stream and kernel alike (profiles/r6/c2_cold_box.jsonl)")
     ap.add_argument("--ceiling", default="on", choices=["on", "off"],
                     help="time a plain read stream over the same frame buffer (tools/libstream_ceiling.so) "
                          "and report the kernel against it (roofline.read_ceiling)")
@@ -883,6 +887,13 @@ def main():
     step_rcs = []
     step = lambda: step_rcs.append(rx_fn(*rx_args))
 
+    # bring the device to its steady state first (untimed; every launch's
+    # return code is still checked below)
+    t_warm = time.perf_counter()
+    while time.perf_counter() - t_warm < args.prewarm_s:
+        for _ in range(50):
+            step()
+        torch.cuda.synchronize()
     ceiling = my_ceiling_us = None
     if args.ceiling == "on":
         # The box's read ceiling on this rank's own frame buffer, measured
