@@ -7,7 +7,7 @@ ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
 LIB      := mtcp_amd/lib/libmtcp_gpu.so
 SRCS     := mtcp_amd/csrc/mtcp_gpu.hip mtcp_amd/csrc/pktgen.hip mtcp_amd/csrc/rxq.hip
-DEPS     := $(SRCS) mtcp_amd/csrc/dispatch.hpp mtcp_amd/csrc/rx_kernels.hpp mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/rx_span.hpp mtcp_amd/csrc/host_copy.hpp mtcp_amd/csrc/park.hpp mtcp_amd/csrc/wait.hpp mtcp_amd/csrc/flow_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h include/mtcp_gpu_rxq.h
+DEPS     := $(SRCS) mtcp_amd/csrc/dispatch.hpp mtcp_amd/csrc/rx_kernels.hpp mtcp_amd/csrc/rx_wave.hpp mtcp_amd/csrc/rx_span.hpp mtcp_amd/csrc/host_copy.hpp mtcp_amd/csrc/park.hpp mtcp_amd/csrc/wait.hpp mtcp_amd/csrc/ctx_internal.hpp mtcp_amd/csrc/flow_kernels.hpp include/mtcp_gpu.h include/mtcp_gpu_pktgen.h include/mtcp_gpu_rxq.h
 
 .PHONY: all lib oracle ref golden examples clean tools
 

@@ -51,8 +51,9 @@ typedef struct mtcp_gpu_rxq mtcp_gpu_rxq;
 int  mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts,
                          uint64_t max_bytes);
 
-/* Free the rxq.  A flush still in flight is waited for (within the wait
- * limit; past it the buffers are left allocated, as below).  After
+/* Free the rxq (before mtcp_gpu_close of its context).  A flush still in
+ * flight is waited for (within the wait limit; past it the buffers are left
+ * allocated, as below).  After
  * mtcp_gpu_rxq_wait_for gave up on a flush (MTCP_GPU_ETIMEDOUT), that flush
  * may still copy into the staging and results: destroy then waits for it at
  * most MTCP_GPU_RXQ_DESTROY_WAIT_US more, and if it still has not finished,

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/mtcp_gpu.h"
+#include "ctx_internal.hpp"
 #include "dispatch.hpp"
 #include "flow_kernels.hpp"
 #include "host_copy.hpp"
@@ -642,6 +643,8 @@ int mtcp_gpu_set_wait_limit(mtcp_gpu_ctx *ctx, uint32_t timeout_us) {
 
 uint32_t mtcp_gpu_wait_limit(const mtcp_gpu_ctx *ctx) { return ctx ? ctx->wait_us : 0u; }
 
+bool mg_ctx_abandoned(const mtcp_gpu_ctx *ctx) { return ctx && ctx->abandoned; }
+
 int mtcp_gpu_reserve(mtcp_gpu_ctx *ctx, uint64_t max_bytes, uint32_t max_pkts) {
     if (!ctx) return MTCP_GPU_EINVAL;
     if (ctx->abandoned) return MTCP_GPU_EIO;
@@ -912,9 +915,11 @@ int rx_host(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len, const mtcp_
         }
     }
     // a stage_collect that timed out has abandoned the context already: no
-    // more waits (finish_call would wait out nothing new, but the call has
-    // reached its deadline)
-    if (rc == MTCP_GPU_ETIMEDOUT) return rc;
+    // more waits, and no stage's records are copied out
+    if (rc == MTCP_GPU_ETIMEDOUT) {
+        for (auto &t : ctx->stage) t.pend_cnt = 0;
+        return rc;
+    }
     return finish_call(ctx, rc, dl, kStages, out_b, rec);
 }
 

@@ -23,6 +23,7 @@
 
 #include "../../include/mtcp_gpu.h"
 #include "../../include/mtcp_gpu_rxq.h"
+#include "ctx_internal.hpp"
 #include "host_copy.hpp"
 #include "park.hpp"
 #include "wait.hpp"
@@ -101,6 +102,7 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
                         uint64_t max_bytes) {
     if (!out || !ctx || !max_pkts || max_bytes < 64) return MTCP_GPU_EINVAL;
     *out = nullptr;
+    if (mg_ctx_abandoned(ctx)) return MTCP_GPU_EIO;   // its stream may never finish
     hipDevice_t dev = 0;
     if (hipStreamGetDevice(reinterpret_cast<hipStream_t>(mtcp_gpu_stream(ctx)), &dev) != hipSuccess)
         return MTCP_GPU_ENODEV;
@@ -140,11 +142,12 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
     const uint64_t h2d = staging < (1ull << 20) ? staging : (1ull << 20);
     const uint64_t d2h = (uint64_t)max_pkts * q->rec;
     memset(q->buf, 0, h2d);
-    if (rc == MTCP_GPU_OK &&
+    const bool queued = rc == MTCP_GPU_OK;
+    if (queued &&
         (hipMemcpyAsync(q->d_buf, q->buf, h2d, hipMemcpyHostToDevice, q->stream) != hipSuccess ||
          hipMemcpyAsync(q->res, q->d_out, d2h, hipMemcpyDeviceToHost, q->stream) != hipSuccess))
         rc = MTCP_GPU_EIO;
-    {
+    if (queued) {
         // (a failed enqueue drains too: a copy already queued uses the staging)
         const int w = mtcp_wait::drain(q->stream, Deadline(q->wait_us));
         if (w == MTCP_GPU_ETIMEDOUT) {
@@ -164,7 +167,7 @@ int mtcp_gpu_rxq_create(mtcp_gpu_rxq **out, mtcp_gpu_ctx *ctx, uint32_t max_pkts
 void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q) {
     if (!q) return;
     RxqDevice dg(q->device);
-    if (q->evt && q->abandoned) {
+    if (q->evt && (q->abandoned || (q->inflight && mg_ctx_abandoned(q->ctx)))) {
         // a flush rxq_wait_for gave up on may still copy into buf / res /
         // d_out: wait for it a bounded time; if the device still has not
         // finished it, leave every buffer and the event allocated (never
@@ -238,7 +241,7 @@ uint32_t mtcp_gpu_rxq_pending(const mtcp_gpu_rxq *q) { return q ? q->n - q->done
 
 int mtcp_gpu_rxq_flush_async(mtcp_gpu_rxq *q) {
     if (!q || q->inflight) return MTCP_GPU_EINVAL;
-    if (q->abandoned) return MTCP_GPU_EIO;
+    if (q->abandoned || mg_ctx_abandoned(q->ctx)) return MTCP_GPU_EIO;
     if (q->n == q->done_n) return MTCP_GPU_OK;
     RxqDevice dg(q->device);
     if (!dg.ok) return MTCP_GPU_ENODEV;
@@ -284,7 +287,11 @@ int mtcp_gpu_rxq_wait_for(mtcp_gpu_rxq *q, uint32_t *n, uint32_t timeout_us) {
     int rc = MTCP_GPU_OK;
     if (q->inflight) {
         RxqDevice dg(q->device);
-        rc = mtcp_wait::wait_event(q->evt, Deadline(timeout_us ? timeout_us : q->wait_us));
+        // (a context abandoned meanwhile, e.g. by a tx fill that timed out on
+        // the same stream, is not waited on: one look at the event)
+        uint32_t lim = timeout_us ? timeout_us : q->wait_us;
+        if (!lim && mg_ctx_abandoned(q->ctx)) lim = 1;
+        rc = mtcp_wait::wait_event(q->evt, Deadline(lim));
         if (rc == MTCP_GPU_OK)
             q->done_n += q->inflight;
         else if (rc == MTCP_GPU_ETIMEDOUT)

@@ -383,3 +383,43 @@ def test_one_threads_stall_does_not_delay_another():
     assert r["a_busy_after_b"], r                          # A's stall outlasted all of B's work
     assert r["b_s"] < 0.3, r
     assert r["a_records_ok"], r                            # and A's aggregate, once its stall ended
+
+
+def test_rxqs_of_an_abandoned_context_do_not_touch_the_device(gpu, golden):
+    """A context abandoned by a tx fill that timed out (its own limit, the
+    context without one) while one of its rxqs has a flush queued behind the
+    same stall: the rxq's wait takes one look and gives up (no unbounded
+    wait on the abandoned stream), its further flushes and a new rxq on the
+    context answer EIO without touching the device, and its destroy returns
+    within its bound while the stall still runs."""
+    from mtcp_amd._lib import MtcpGpuError, lib
+    L, T = lib(), stall_lib()
+    ctx = gpu.Context(0)
+    handle = ctx.stream
+    base = golden.buf.ctypes.data
+    q = ctypes.c_void_p()
+    assert L.mtcp_gpu_rxq_create(ctypes.byref(q), ctx._h, 256, 256 * 2048) == 0
+    for d in golden.desc[:256]:
+        assert L.mtcp_gpu_rxq_push(q, base + int(d["offset"]), int(d["len"])) == 0
+    assert T.mtcp_gpu_debug_stall(ctx._h, STALL_US) == 0
+    assert L.mtcp_gpu_rxq_flush_async(q) == 0
+    part = golden.desc[:64]
+    host = golden.buf.copy()
+    with pytest.raises(MtcpGpuError) as e:
+        ctx.tx_fill_ptrs(host, part["offset"].astype(np.int64), part["len"], timeout_us=LIMIT_US)
+    assert e.value.code == ETIMEDOUT
+    t0 = time.monotonic()
+    n = ctypes.c_uint32(7)
+    assert L.mtcp_gpu_rxq_wait(q, ctypes.byref(n)) == ETIMEDOUT        # one look, no wait
+    assert time.monotonic() - t0 < SLACK_S
+    assert n.value == 0 and stream_busy(handle)
+    assert L.mtcp_gpu_rxq_flush_async(q) == EIO
+    q2 = ctypes.c_void_p()
+    assert L.mtcp_gpu_rxq_create(ctypes.byref(q2), ctx._h, 64, 64 * 2048) == EIO
+    t0 = time.monotonic()
+    L.mtcp_gpu_rxq_destroy(q)
+    assert time.monotonic() - t0 < 0.1 + SLACK_S                       # MTCP_GPU_RXQ_DESTROY_WAIT_US
+    assert stream_busy(handle)
+    ctx.close()
+    stream_wait(handle)
+    assert np.array_equal(host, golden.buf)                             # the tx fill wrote nothing
