@@ -29,7 +29,7 @@ golden:
 	$(MAKE) -C oracle golden
 
 clean:
-	rm -f $(LIB) tests/c/libmtcp_gpu_testing.so tests/c/rxloop tests/c/admit_test tools/libstream_ceiling.so
+	rm -f $(LIB) tests/c/libmtcp_gpu_testing.so tests/c/rxloop tests/c/admit_test tests/c/park_test tools/libstream_ceiling.so
 	$(MAKE) -C oracle clean
 
 # the probe tools instantiate rx_kernel's profiling / timing-probe variants
@@ -63,6 +63,10 @@ tests/c/rxloop: tests/c/rxloop.c mtcp_amd/io_module/gpu_module.c mtcp_amd/io_mod
 	gcc -std=gnu99 -O3 -Wall -pthread -DMTCP_GPU_TESTING -Itests/c/mtcp_double -Itests/c -Iinclude -o $@ tests/c/rxloop.c \
 	    mtcp_amd/io_module/gpu_module.c oracle/mtcp_oracle.c -Lmtcp_amd/lib -Ltests/c -lmtcp_gpu -lmtcp_gpu_testing -ldl \
 	    -Wl,-rpath,'$$ORIGIN/../../mtcp_amd/lib' -Wl,-rpath,'$$ORIGIN'
+
+# park.hpp's best fit and caps, run on the GPU box (tests/test_gpu_bounded.py)
+tests/c/park_test: tests/c/park_test.hip mtcp_amd/csrc/park.hpp
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Wall -o $@ $<
 
 # the admission / limit logic of gpu_module.c, unit-tested on the CPU
 tests/c/admit_test: tests/c/admit_test.c mtcp_amd/io_module/gpu_module.c $(LIB)

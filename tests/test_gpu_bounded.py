@@ -423,3 +423,22 @@ def test_rxqs_of_an_abandoned_context_do_not_touch_the_device(gpu, golden):
     ctx.close()
     stream_wait(handle)
     assert np.array_equal(host, golden.buf)                             # the tx fill wrote nothing
+
+
+def test_park_best_fit():
+    """park.hpp hands a parked buffer to the smallest
+    request it covers up to twice over (a sweep of sizes reuses what it
+    parked), a buffer handed out larger than asked goes back with its real
+    size, pinned host and device buffers stay apart, and a buffer above
+    kParkMaxBytes is freed rather than parked (tests/c/park_test.hip)."""
+    import json
+    import subprocess
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    p = subprocess.run([os.path.join(ROOT, "tests", "c", "park_test")], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["ok"] and r["best_fit_reused"] and r["small_not_reused"] and r["real_size_kept"], r
+    assert r["smallest_wins"] and r["kinds_apart"] and r["big_freed"], r
+    assert r["parked_after_release"] == 1 << 20 and r["parked_after_reuse"] == 0, r
+    assert r["parked_after_lent_release"] == 1 << 20, r                 # its real size, not the 700 KiB asked
