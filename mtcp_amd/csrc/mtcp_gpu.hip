@@ -306,22 +306,23 @@ hipStream_t pick(mtcp_gpu_ctx *ctx, void *stream) {
     return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
 }
 
-// a stage's buffers back to park.hpp (its stream has no work on them)
-void stage_release_buf(Stage &s) {
-    mtcp_park::release(s.d_buf, s.buf_cap, mtcp_park::kDevice);
+// a stage's buffers back to park.hpp (its stream has no work on them);
+// may_free = false inside a bounded call: nothing may wait on the device
+void stage_release_buf(Stage &s, bool may_free) {
+    mtcp_park::release(s.d_buf, s.buf_cap, mtcp_park::kDevice, may_free);
     s.d_buf = nullptr;
     s.buf_cap = 0;
 }
-void stage_release_pkts(Stage &s) {
-    mtcp_park::release(s.d_desc, (size_t)s.pkt_cap * sizeof(mtcp_gpu_desc), mtcp_park::kDevice);
-    mtcp_park::release(s.d_out, (size_t)s.pkt_cap * sizeof(mtcp_gpu_result), mtcp_park::kDevice);
+void stage_release_pkts(Stage &s, bool may_free) {
+    mtcp_park::release(s.d_desc, (size_t)s.pkt_cap * sizeof(mtcp_gpu_desc), mtcp_park::kDevice, may_free);
+    mtcp_park::release(s.d_out, (size_t)s.pkt_cap * sizeof(mtcp_gpu_result), mtcp_park::kDevice, may_free);
     s.d_desc = nullptr;
     s.d_out = nullptr;
     s.pkt_cap = 0;
 }
-void stage_release_host(Stage &s) {
-    mtcp_park::release(s.h_in, s.h_in_cap, mtcp_park::kHost);
-    mtcp_park::release(s.h_out, s.h_out_cap, mtcp_park::kHost);
+void stage_release_host(Stage &s, bool may_free) {
+    mtcp_park::release(s.h_in, s.h_in_cap, mtcp_park::kHost, may_free);
+    mtcp_park::release(s.h_out, s.h_out_cap, mtcp_park::kHost, may_free);
     s.h_in = s.h_out = nullptr;
     s.h_in_cap = s.h_out_cap = 0;
 }
@@ -356,17 +357,17 @@ int stage_reserve(mtcp_gpu_ctx *ctx, Stage &s, uint64_t bytes, uint32_t pkts, co
     if ((bytes > s.buf_cap || pkts > s.pkt_cap) && (rc = waited(ctx, drain(s.stream, dl))) != MTCP_GPU_OK)
         return rc;
     if (bytes > s.buf_cap) {
-        stage_release_buf(s);
+        stage_release_buf(s, !dl.bounded);
         const uint64_t cap = (bytes + 4095) & ~4095ull;
         if (!HIP_OK(mtcp_park::alloc(&s.d_buf, cap, mtcp_park::kDevice))) return MTCP_GPU_ENOMEM;
         s.buf_cap = cap;
     }
     if (pkts > s.pkt_cap) {
-        stage_release_pkts(s);
+        stage_release_pkts(s, !dl.bounded);
         if (!HIP_OK(mtcp_park::alloc(&s.d_desc, (size_t)pkts * sizeof(mtcp_gpu_desc), mtcp_park::kDevice)))
             return MTCP_GPU_ENOMEM;
         if (!HIP_OK(mtcp_park::alloc(&s.d_out, (size_t)pkts * sizeof(mtcp_gpu_result), mtcp_park::kDevice))) {
-            mtcp_park::release(s.d_desc, (size_t)pkts * sizeof(mtcp_gpu_desc), mtcp_park::kDevice);
+            mtcp_park::release(s.d_desc, (size_t)pkts * sizeof(mtcp_gpu_desc), mtcp_park::kDevice, !dl.bounded);
             s.d_desc = nullptr;
             return MTCP_GPU_ENOMEM;
         }
@@ -384,7 +385,7 @@ int stage_host(mtcp_gpu_ctx *ctx, Stage &s, uint64_t in_bytes, uint64_t out_byte
         (rc = waited(ctx, drain(s.stream, dl))) != MTCP_GPU_OK)
         return rc;
     if (in_bytes > s.h_in_cap) {
-        mtcp_park::release(s.h_in, s.h_in_cap, mtcp_park::kHost);
+        mtcp_park::release(s.h_in, s.h_in_cap, mtcp_park::kHost, !dl.bounded);
         s.h_in = nullptr;
         s.h_in_cap = 0;
         const uint64_t cap = (in_bytes + 4095) & ~4095ull;
@@ -392,7 +393,7 @@ int stage_host(mtcp_gpu_ctx *ctx, Stage &s, uint64_t in_bytes, uint64_t out_byte
         s.h_in_cap = cap;
     }
     if (out_bytes > s.h_out_cap) {
-        mtcp_park::release(s.h_out, s.h_out_cap, mtcp_park::kHost);
+        mtcp_park::release(s.h_out, s.h_out_cap, mtcp_park::kHost, !dl.bounded);
         s.h_out = nullptr;
         s.h_out_cap = 0;
         const uint64_t cap = (out_bytes + 4095) & ~4095ull;
@@ -621,16 +622,18 @@ void mtcp_gpu_close(mtcp_gpu_ctx *ctx) {
         return;
     }
     // every buffer goes back to park.hpp: a free here would wait for the
-    // other contexts' work on the device
+    // other contexts' work on the device (with a wait limit not even a
+    // buffer too large to park is freed)
+    const bool may_free = ctx->wait_us == 0;
     for (auto &s : ctx->stage) {
         if (s.own_stream) (void)hipStreamDestroy(s.stream);
-        stage_release_buf(s);
-        stage_release_pkts(s);
-        stage_release_host(s);
+        stage_release_buf(s, may_free);
+        stage_release_pkts(s, may_free);
+        stage_release_host(s, may_free);
     }
-    mtcp_park::release(ctx->h_gather, ctx->h_gather_cap, mtcp_park::kHost);
+    mtcp_park::release(ctx->h_gather, ctx->h_gather_cap, mtcp_park::kHost, may_free);
     mtcp_park::release(ctx->h_gather_desc, (size_t)ctx->h_gather_desc_cap * sizeof(mtcp_gpu_desc),
-                       mtcp_park::kHost);
+                       mtcp_park::kHost, may_free);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -926,12 +929,13 @@ int rx_host(mtcp_gpu_ctx *ctx, const uint8_t *buf, uint64_t buf_len, const mtcp_
 // Gather a pointer burst into the context's pinned PSIO-style chunk (64 B
 // aligned slots, pslib.c:146) with its descriptors; *total = chunk bytes.
 int gather_burst(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *lens, uint32_t n,
-                 uint64_t *total_out) {
+                 uint64_t *total_out, const Deadline &dl) {
     if (ctx->abandoned) return MTCP_GPU_EIO;     // its staging may still be under DMA
+    const bool may_free = !dl.bounded;
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) total += ((uint64_t)lens[i] + 63) & ~63ull;
     if (total > ctx->h_gather_cap) {
-        mtcp_park::release(ctx->h_gather, ctx->h_gather_cap, mtcp_park::kHost);
+        mtcp_park::release(ctx->h_gather, ctx->h_gather_cap, mtcp_park::kHost, may_free);
         ctx->h_gather = nullptr;
         ctx->h_gather_cap = 0;
         if (!HIP_OK(mtcp_park::alloc(&ctx->h_gather, total, mtcp_park::kHost))) return MTCP_GPU_ENOMEM;
@@ -939,7 +943,7 @@ int gather_burst(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16_t *
     }
     if (n > ctx->h_gather_desc_cap) {
         mtcp_park::release(ctx->h_gather_desc, (size_t)ctx->h_gather_desc_cap * sizeof(mtcp_gpu_desc),
-                           mtcp_park::kHost);
+                           mtcp_park::kHost, may_free);
         ctx->h_gather_desc = nullptr;
         ctx->h_gather_desc_cap = 0;
         if (!HIP_OK(mtcp_park::alloc(&ctx->h_gather_desc, (size_t)n * sizeof(mtcp_gpu_desc), mtcp_park::kHost)))
@@ -992,7 +996,7 @@ int mtcp_gpu_rx_ptrs(mtcp_gpu_ctx *ctx, const uint8_t *const *pkts, const uint16
     DeviceGuard dg(ctx->device);
     const Deadline dl(ctx->wait_us);
     uint64_t total = 0;
-    const int rc = gather_burst(ctx, pkts, lens, n, &total);
+    const int rc = gather_burst(ctx, pkts, lens, n, &total, dl);
     if (rc != MTCP_GPU_OK) return rc;
     return rx_host(ctx, ctx->h_gather, total, ctx->h_gather_desc, n, 6, out, true, dl);
 }
@@ -1016,7 +1020,7 @@ int mtcp_gpu_tx_fill_ptrs_for(mtcp_gpu_ctx *ctx, uint8_t *const *pkts, const uin
     DeviceGuard dg(ctx->device);
     const Deadline dl(timeout_us ? timeout_us : ctx->wait_us);
     uint64_t total = 0;
-    int rc = gather_burst(ctx, pkts, lens, n, &total);
+    int rc = gather_burst(ctx, pkts, lens, n, &total, dl);
     if (rc != MTCP_GPU_OK) return rc;
     Stage &s = ctx->stage[0];
     rc = stage_reserve(ctx, s, ((total + 15) & ~15ull) + 16, n, dl);
@@ -1253,7 +1257,7 @@ int mtcp_gpu_addr_pool_search(mtcp_gpu_ctx *ctx, int core, int num_queues, uint3
     }
     if (rc == MTCP_GPU_ETIMEDOUT) return rc;                 // abandoned: d_mem stays allocated
     if (rc != MTCP_GPU_OK) (void)finish_call(ctx, rc, dl, 1);
-    if (!ctx->abandoned) mtcp_park::release(d_mem, bytes, mtcp_park::kDevice);
+    if (!ctx->abandoned) mtcp_park::release(d_mem, bytes, mtcp_park::kDevice, !dl.bounded);
     return rc;
 }
 

@@ -16,7 +16,9 @@
 //
 // Bounds: buffers above kParkMaxBytes (a bench-sized reserve) are freed as
 // before, and at most kParkDeviceBytes of each kind (pinned host, device)
-// are parked per device (past that a release frees).  A parked buffer is
+// are parked per device (past that a release frees) — except for a release
+// that must not wait (a call bounded by a context wait limit), which parks
+// whatever the size.  A parked buffer is
 // handed to the smallest request it covers up to twice over (best fit), so
 // that a process whose sizes vary (a sweep of rxq sizes, the tests) reuses
 // what it parked instead of filling the park with sizes that never match
@@ -67,7 +69,7 @@ inline int current_device() {
 inline hipError_t alloc(void **out, size_t bytes, Kind kind) {
     *out = nullptr;
     const int dev = current_device();
-    if (dev >= 0 && dev < kParkDevices && bytes <= kParkMaxBytes) {
+    if (dev >= 0 && dev < kParkDevices) {
         Pool &pl = pool();
         std::lock_guard<std::mutex> lk(pl.m);
         size_t best = pl.bufs.size();
@@ -98,8 +100,11 @@ inline hipError_t alloc(T **out, size_t bytes, Kind kind) {
     return e;
 }
 
-// give back a buffer alloc() returned (with the size it was asked for)
-inline void release(void *p, size_t bytes, Kind kind) {
+// give back a buffer alloc() returned (with the size it was asked for).
+// may_free = false: the caller must not wait on the device (a call bounded
+// by a context wait limit), so the buffer is parked whatever its size and
+// the caps — a free here would wait for every stream on the device.
+inline void release(void *p, size_t bytes, Kind kind, bool may_free = true) {
     if (!p) return;
     const int dev = current_device();
     Pool &pl = pool();
@@ -112,8 +117,8 @@ inline void release(void *p, size_t bytes, Kind kind) {
                 pl.lent.pop_back();
                 break;
             }
-        if (dev >= 0 && dev < kParkDevices && bytes <= kParkMaxBytes &&
-            pl.parked[dev][kind] + bytes <= kParkDeviceBytes) {
+        if (dev >= 0 && dev < kParkDevices &&
+            (!may_free || (bytes <= kParkMaxBytes && pl.parked[dev][kind] + bytes <= kParkDeviceBytes))) {
             pl.bufs.push_back({dev, kind, bytes, p});
             pl.parked[dev][kind] += bytes;
             return;

@@ -195,11 +195,13 @@ void mtcp_gpu_rxq_destroy(mtcp_gpu_rxq *q) {
     }
     // parked, not freed (park.hpp): hipFree / hipHostFree would wait for
     // every stream on the device, other threads' hung work included
-    mtcp_park::release(q->buf, q->staging, mtcp_park::kHost);
-    mtcp_park::release(q->desc, (size_t)q->max_pkts * sizeof(mtcp_gpu_desc), mtcp_park::kHost);
-    mtcp_park::release(q->res, (size_t)q->max_pkts * q->rec, mtcp_park::kHost);
-    mtcp_park::release(q->d_buf, q->staging, mtcp_park::kDevice);
-    mtcp_park::release(q->d_out, (size_t)q->max_pkts * q->rec, mtcp_park::kDevice);
+    // (with a wait limit not even a buffer too large to park is freed)
+    const bool may_free = q->wait_us == 0;
+    mtcp_park::release(q->buf, q->staging, mtcp_park::kHost, may_free);
+    mtcp_park::release(q->desc, (size_t)q->max_pkts * sizeof(mtcp_gpu_desc), mtcp_park::kHost, may_free);
+    mtcp_park::release(q->res, (size_t)q->max_pkts * q->rec, mtcp_park::kHost, may_free);
+    mtcp_park::release(q->d_buf, q->staging, mtcp_park::kDevice, may_free);
+    mtcp_park::release(q->d_out, (size_t)q->max_pkts * q->rec, mtcp_park::kDevice, may_free);
     delete q;
 }
 

@@ -54,10 +54,21 @@ int main() {
     ok &= alloc(&big, mtcp_park::kParkMaxBytes + MiB, kDevice) == hipSuccess;
     release(big, mtcp_park::kParkMaxBytes + MiB, kDevice);
     const int big_freed = parked(0, kDevice) == before_big;
+    // ... unless the release must not wait (a bounded call): parked anyway,
+    // and the next request of that size gets it back
+    void *big2 = nullptr, *big3 = nullptr;
+    const size_t bigsz = mtcp_park::kParkMaxBytes + MiB;
+    ok &= alloc(&big2, bigsz, kDevice) == hipSuccess;
+    release(big2, bigsz, kDevice, /*may_free=*/false);
+    const int big_parked_when_bounded = parked(0, kDevice) == before_big + bigsz;
+    ok &= alloc(&big3, bigsz, kDevice) == hipSuccess;
+    const int big_reused = big3 == big2;
+    release(big3, bigsz, kDevice);
     printf("{\"ok\": %d, \"best_fit_reused\": %d, \"small_not_reused\": %d, \"real_size_kept\": %d, "
-           "\"smallest_wins\": %d, \"kinds_apart\": %d, \"big_freed\": %d, \"parked_after_release\": %zu, "
+           "\"smallest_wins\": %d, \"kinds_apart\": %d, \"big_freed\": %d, \"big_parked_when_bounded\": %d, "
+           "\"big_reused\": %d, \"parked_after_release\": %zu, "
            "\"parked_after_reuse\": %zu, \"parked_after_lent_release\": %zu}\n",
-           ok, best_fit_reused, small_not_reused, real_size_kept, smallest_wins, kinds_apart, big_freed, p0, p1,
-           p2);
+           ok, best_fit_reused, small_not_reused, real_size_kept, smallest_wins, kinds_apart, big_freed,
+           big_parked_when_bounded, big_reused, p0, p1, p2);
     return 0;
 }

@@ -430,7 +430,9 @@ def test_park_best_fit():
     request it covers up to twice over (a sweep of sizes reuses what it
     parked), a buffer handed out larger than asked goes back with its real
     size, pinned host and device buffers stay apart, and a buffer above
-    kParkMaxBytes is freed rather than parked (tests/c/park_test.hip)."""
+    kParkMaxBytes is freed rather than parked — unless the release belongs
+    to a call bounded by a wait limit, which must not wait on the device:
+    then it is parked and reused (tests/c/park_test.hip)."""
     import json
     import subprocess
     if not torch.cuda.is_available():
@@ -440,5 +442,6 @@ def test_park_best_fit():
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["ok"] and r["best_fit_reused"] and r["small_not_reused"] and r["real_size_kept"], r
     assert r["smallest_wins"] and r["kinds_apart"] and r["big_freed"], r
+    assert r["big_parked_when_bounded"] and r["big_reused"], r          # a bounded call never frees
     assert r["parked_after_release"] == 1 << 20 and r["parked_after_reuse"] == 0, r
     assert r["parked_after_lent_release"] == 1 << 20, r                 # its real size, not the 700 KiB asked
