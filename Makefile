@@ -29,7 +29,7 @@ golden:
 	$(MAKE) -C oracle golden
 
 clean:
-	rm -f $(LIB) tests/c/libmtcp_gpu_testing.so tests/c/rxloop tests/c/admit_test tests/c/park_test tools/libstream_ceiling.so
+	rm -f $(LIB) tests/c/libmtcp_gpu_testing.so tests/c/rxloop tests/c/admit_test tests/c/park_test tests/c/asan_host tools/libstream_ceiling.so
 	$(MAKE) -C oracle clean
 
 # the probe tools instantiate rx_kernel's profiling / timing-probe variants
@@ -67,6 +67,13 @@ tests/c/rxloop: tests/c/rxloop.c mtcp_amd/io_module/gpu_module.c mtcp_amd/io_mod
 # park.hpp's best fit and caps, run on the GPU box (tests/test_gpu_bounded.py)
 tests/c/park_test: tests/c/park_test.hip mtcp_amd/csrc/park.hpp
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Wall -o $@ $<
+
+# the C ABI's host code under AddressSanitizer (host side only: the pool has
+# no GPU ASan), run on the GPU box by tests/test_gpu_bounded.py
+ASAN_SRCS := tests/c/asan_host.hip mtcp_amd/csrc/mtcp_gpu.hip mtcp_amd/csrc/rxq.hip mtcp_amd/csrc/pktgen.hip
+tests/c/asan_host: $(ASAN_SRCS) $(DEPS)
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -g -std=c++17 -Wall -Wno-unused-result -Xarch_host -fsanitize=address \
+	    -Xarch_host -fno-omit-frame-pointer -o $@ $(ASAN_SRCS)
 
 # the admission / limit logic of gpu_module.c, unit-tested on the CPU
 tests/c/admit_test: tests/c/admit_test.c mtcp_amd/io_module/gpu_module.c $(LIB)

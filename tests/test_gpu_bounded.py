@@ -445,3 +445,27 @@ def test_park_best_fit():
     assert r["big_parked_when_bounded"] and r["big_reused"], r          # a bounded call never frees
     assert r["parked_after_release"] == 1 << 20 and r["parked_after_reuse"] == 0, r
     assert r["parked_after_lent_release"] == 1 << 20, r                 # its real size, not the 700 KiB asked
+
+
+def test_host_code_under_asan_on_the_gpu(golden):
+    """The C ABI's host code — staging, bounce buffers, gathers, parking,
+    rxqs, bounded waits — built with AddressSanitizer on the host side
+    (tests/c/asan_host.hip; the pool has no GPU ASan) and driven on the
+    MI355X through every host entry point without and with a wait limit,
+    over a multi-stage chunk, and through each bounded call giving up
+    behind a stall: no ASan report, bounded and unbounded calls write the
+    same bytes, every bounded call behind the stall answers ETIMEDOUT and
+    leaves the caller's buffers untouched after the stall ends."""
+    import json
+    import subprocess
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    gold = os.path.join(ROOT, "tests", "golden")
+    p = subprocess.run([os.path.join(ROOT, "tests", "c", "asan_host"), os.path.join(gold, "rx_buf.bin"),
+                        os.path.join(gold, "rx_desc.bin")], capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0"))
+    assert "AddressSanitizer" not in p.stderr, p.stderr[-3000:]
+    assert p.returncode == 0, p.stdout[-1000:] + p.stderr[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["ok"] and r["bounded_equals_unbounded"] and r["timeouts"] == 7, r
+    assert r["frames"] == len(golden.desc)
